@@ -1,0 +1,146 @@
+/*
+ * kb2e_engine.h -- the drop-in C ABI of the kb2e_amd MI355X training engine.
+ *
+ * The reference (eriq-augustine/KB2E) runs its per-triple SGD hot path inside
+ * the C++ class common::Trainer (common/trainer.h:14-78).  Its protected
+ * virtual bfgs() (common/trainer.h:59, common/trainer.cpp:69-107) loops over
+ * epochs and batches, draws a corrupted triple per sample, scores both triples
+ * with the model's tripleEnergy() and applies gradientUpdate() to the *_next_
+ * tables (transe/trainer.cpp:25-56, transh/trainer.cpp:11-75,
+ * transr/trainer.cpp:35-188).  This ABI replaces exactly that loop: a host
+ * trainer overrides bfgs() and calls the functions below (INTEGRATION.md shows
+ * the binding).  Everything else (argument parsing, file loading, writing the
+ * embedding text files, evaluation binaries) stays on the host.
+ *
+ * Conventions: plain C types, caller-owned buffers borrowed only for the call,
+ * row-major contiguous tables, status codes instead of exceptions.  One host
+ * thread per context; contexts are independent (one per GPU / rank).
+ */
+#ifndef KB2E_ENGINE_H_
+#define KB2E_ENGINE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    KB2E_OK = 0,
+    KB2E_EINVAL = 1,      /* bad argument / shape (reference: printf + exit(1)) */
+    KB2E_EDEVICE = 2,     /* HIP runtime or kernel failure */
+    KB2E_ESTATE = 3,      /* call order violated (e.g. train before upload) */
+    KB2E_ENOMEM = 4,
+    KB2E_EUNSUPPORTED = 5,
+    KB2E_ESAMPLER = 6     /* a negative could not be drawn (every entity is a
+                             known triple: the reference loops forever here,
+                             common/trainer.cpp:89-96) */
+} kb2e_status;
+
+typedef enum { KB2E_TRANSE = 0, KB2E_TRANSH = 1, KB2E_TRANSR = 2 } kb2e_model;
+
+/* Where the sample stream (train index i, corrupting entity j, side) comes from. */
+typedef enum {
+    KB2E_SAMPLER_GLIBC = 0,  /* the reference's own stream: glibc TYPE_3 rand()
+                                seeded by `seed`, consumed exactly as
+                                common/trainer.cpp:79-98 (default) */
+    KB2E_SAMPLER_REPLAY = 1  /* caller supplies the stream (kb2e_set_sample_stream) */
+} kb2e_sampler;
+
+typedef struct {
+    int32_t model;          /* kb2e_model */
+    int32_t dim;            /* --size (common/args.cpp:71-74) */
+    int32_t num_entities;
+    int32_t num_relations;
+    double learning_rate;   /* --rate */
+    double margin;          /* --margin */
+    int32_t method;         /* 0 unif, 1 bern (common/constants.h:7-8) */
+    int32_t distance;       /* 0 L1, 1 L2 (common/constants.h:16-17); TransH is always L1 */
+    int32_t num_batches;    /* --batches */
+    uint32_t seed;          /* --seed: srand() in main (transe/bin/trainTransE.cpp:13) */
+    int32_t precision;      /* 64 = FP64 tables and arithmetic like the reference; 32 = FP32 */
+    int32_t sampler;        /* kb2e_sampler */
+    int32_t transr_compat;  /* 1: reproduce the accumulating TransR energy of
+                               transr/transr.cpp:20-25; 0: zeroed work vectors */
+    int32_t device;         /* HIP device ordinal */
+} kb2e_config;
+
+typedef struct kb2e_ctx kb2e_ctx;
+
+/* Fill `cfg` with the reference defaults (common/constants.h:28-40). */
+void kb2e_default_config(kb2e_config* cfg);
+
+kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out);
+void kb2e_destroy(kb2e_ctx* ctx);
+const char* kb2e_last_error(const kb2e_ctx* ctx);
+
+/* Trainer::add for every training triple, in train-file order, plus the
+ * per-relation head/tail co-occurrence means of Trainer::loadFiles
+ * (common/trainer.cpp:26-32, 151-201).  Builds the negative-sample filter and
+ * the Bernoulli table on the device. */
+kb2e_status kb2e_upload_triples(kb2e_ctx* ctx, const int32_t* heads, const int32_t* tails,
+                                const int32_t* relations, int64_t count);
+
+/* Trainer::prepTrain (common/trainer.cpp:34-58; transh/trainer.cpp:77-88;
+ * transr/trainer.cpp:70-86 up to the seed files): draws the initial tables from
+ * the context's glibc stream exactly as the reference does, uploads them, and
+ * (if the pointers are non-NULL) returns them.  Weights: TransH R x n, TransR
+ * R x n x n ([r][j][i]). */
+kb2e_status kb2e_init_params(kb2e_ctx* ctx, double* entity, double* relation, double* weights);
+
+/* Upload tables (row-major FP64 as in the reference's vectors).  `weights` may
+ * be NULL for TransE.  Used for TransR seeding (transr/trainer.cpp:88-113; the
+ * caller applies the entity unit norm as the reference does) and for restarts. */
+kb2e_status kb2e_upload_params(kb2e_ctx* ctx, const double* entity, const double* relation,
+                               const double* weights);
+kb2e_status kb2e_download_params(kb2e_ctx* ctx, double* entity, double* relation, double* weights);
+
+/* TransR energy work vectors (transr/trainer.h:28-29), for compat-mode state. */
+kb2e_status kb2e_get_transr_work(kb2e_ctx* ctx, double* head_work, double* tail_work);
+kb2e_status kb2e_set_transr_work(kb2e_ctx* ctx, const double* head_work, const double* tail_work);
+
+/* KB2E_SAMPLER_REPLAY: the next `count` samples (i = train index, j = entity,
+ * side = 1 corrupt tail / 0 corrupt head).  Consumed batch by batch. */
+kb2e_status kb2e_set_sample_stream(kb2e_ctx* ctx, const int32_t* i, const int32_t* j,
+                                   const uint8_t* side, int64_t count);
+
+/* One epoch of Trainer::bfgs (common/trainer.cpp:72-106): numBatches batches of
+ * floor(|train| / numBatches) samples.  *loss = the epoch loss the reference
+ * prints at :105; *active = hinge-active samples.  Either pointer may be NULL. */
+kb2e_status kb2e_train_epoch(kb2e_ctx* ctx, double* loss, int64_t* active);
+
+/* `nbatches` batches continuing the current epoch position (wrapping into the
+ * next epoch).  Asynchronous: returns once queued; results land at the next
+ * kb2e_synchronize / kb2e_epoch_stats. */
+kb2e_status kb2e_train_batches(kb2e_ctx* ctx, int32_t nbatches);
+kb2e_status kb2e_synchronize(kb2e_ctx* ctx);
+/* Loss and active count accumulated since the last call (resets them). */
+kb2e_status kb2e_take_stats(kb2e_ctx* ctx, double* loss, int64_t* active);
+
+/* Raw glibc stream access (the context's RNG, as std::rand() in the reference). */
+int32_t kb2e_rng_next(kb2e_ctx* ctx);
+
+/* Timing of the engine's device kernels on the engine's own HIP stream (HIP
+ * events around each launch; off by default).  `name` is a kernel family
+ * ("score", "fold", "index", "sample", ...).  Returns total milliseconds and
+ * launch count since kb2e_profile_enable(ctx, 1). */
+kb2e_status kb2e_profile_enable(kb2e_ctx* ctx, int32_t on);
+kb2e_status kb2e_profile_query(kb2e_ctx* ctx, const char* name, double* total_ms, int64_t* launches);
+
+/* Device memory footprint in bytes (tables + work buffers). */
+int64_t kb2e_device_bytes(const kb2e_ctx* ctx);
+
+/* Multi-GPU (one context per rank): raw device pointers of the parameter
+ * tables and their element counts, so a communicator (RCCL via
+ * torch.distributed) can reduce deltas in place; kb2e_merge_epoch re-applies
+ * the reference's norm constraints after a merge. */
+kb2e_status kb2e_device_tables(kb2e_ctx* ctx, void** entity, void** relation, void** weights,
+                               int64_t* n_entity, int64_t* n_relation, int64_t* n_weights);
+kb2e_status kb2e_renormalize(kb2e_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KB2E_ENGINE_H_ */

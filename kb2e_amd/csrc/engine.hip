@@ -1,0 +1,809 @@
+// engine.hip -- kb2e_amd training engine: C ABI (include/kb2e_engine.h) and
+// per-epoch orchestration on one MI355X.
+//
+// Per epoch (Trainer::bfgs, common/trainer.cpp:69-107):
+//   1. sample stream: the reference's exact glibc stream (host sampler) or a
+//      replayed one, uploaded once per epoch;
+//   2. event index: one key per (row, sample, update) event, radix-sorted by
+//      (batch, row, sample) and cut into per-row segments (kernels_index.hpp);
+//   3. per batch: phase A (score: energies, hinge, update directions from the
+//      start-of-batch tables) then phase B (ordered per-row folds for TransE;
+//      relation-owner schedule for TransH/TransR) -- the reference's
+//      prebatch/postbatch snapshot semantics without any table copies.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/kb2e_engine.h"
+#include "glibc_rand.hpp"
+#include "host_data.hpp"
+#include "kernels_common.hpp"
+#include "kernels_index.hpp"
+#include "kernels_transe.hpp"
+#include "kernels_relowner.hpp"
+
+using namespace kb2e;
+
+namespace {
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+#define HIPCHK(expr)                                                                              \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess)                                                                     \
+            throw HipError(std::string(#expr) + ": " + hipGetErrorString(_e) + " @" +             \
+                           std::to_string(__LINE__));                                             \
+    } while (0)
+
+int bits_for(int64_t v) {  // bits to hold values 0..v
+    int b = 1;
+    while ((1ll << b) <= v) ++b;
+    return b;
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void alloc(size_t b) {
+        free();
+        if (b == 0) b = 16;
+        HIPCHK(hipMalloc(&p, b));
+        bytes = b;
+    }
+    void free() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const { return (T*)p; }
+    ~DevBuf() { free(); }
+};
+
+struct Timer {
+    double ms = 0;
+    int64_t launches = 0;
+};
+
+}  // namespace
+
+struct kb2e_ctx;
+namespace {
+void setup_relowner_buffers(kb2e_ctx* c);
+template <typename T>
+void run_batch_relowner(kb2e_ctx* c, int64_t b);
+}  // namespace
+
+struct kb2e_ctx {
+    kb2e_config cfg{};
+    std::string err;
+    GlibcRand rng{1};
+    TripleStore ts;
+    bool have_triples = false, have_params = false;
+    int n = 0, ld = 0, ch = 1, nw = 2, esize = 8;
+    int64_t B = 0, nb = 0, S = 0;
+    hipStream_t stream = nullptr;
+    int64_t device_bytes = 0;
+
+    // tables (real_t = double or float by cfg.precision)
+    DevBuf ent, rel, w;
+    int64_t w_elems = 0;  // logical elements (TransH R*n, TransR R*n*n)
+    // triples
+    DevBuf heads, tails, rels;
+    // epoch sample stream
+    DevBuf si, sj, side;
+    std::vector<int32_t> h_si, h_sj;
+    std::vector<uint8_t> h_side;
+    int32_t* pin_si = nullptr;
+    int32_t* pin_sj = nullptr;
+    uint8_t* pin_side = nullptr;
+    // replay stream supplied by the caller
+    std::vector<int32_t> rp_si, rp_sj;
+    std::vector<uint8_t> rp_side;
+    int64_t rp_pos = 0;
+    // event index
+    KeyLayout kl{};
+    int slots = 6;
+    DevBuf keys, keys_sorted, sort_tmp, flags, idx, seg_start, nseg, nvalid, batch_seg;
+    size_t sort_tmp_bytes = 0, scan_tmp_bytes = 0;
+    // phase A outputs
+    DevBuf act, loss;      // [S]
+    DevBuf xbits, xreal;   // [B][2][nw], [B][2][ld]
+    DevBuf aux;            // model-specific per-update exports
+    // relation-owner schedule (TransH / TransR)
+    RelOwnerPlan plan;
+    DevBuf owner, tickets, ent_done, wsnap, transr_work;
+    // stats
+    DevBuf stats;  // double loss, double active (reduced)
+    double acc_loss = 0;
+    int64_t acc_active = 0;
+    int64_t reduced_upto = 0;  // samples of the current epoch already reduced
+    // position
+    int64_t epoch_pos = 0;  // next batch within the epoch
+    bool epoch_ready = false;
+    // profiling
+    bool prof = false;
+    std::map<std::string, Timer> timers;
+    struct Pending {
+        std::string name;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> event_pool;
+
+    ~kb2e_ctx() {
+        if (pin_si) (void)hipHostFree(pin_si);
+        if (pin_sj) (void)hipHostFree(pin_sj);
+        if (pin_side) (void)hipHostFree(pin_side);
+        flush_timers();
+        for (auto e : event_pool) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    bool f64() const { return cfg.precision == 64; }
+
+    hipEvent_t get_event() {
+        if (!event_pool.empty()) {
+            hipEvent_t e = event_pool.back();
+            event_pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        return e;
+    }
+
+    // Bracket a launch with events on the engine stream (when profiling).
+    template <class F>
+    void timed(const char* name, F&& f) {
+        if (!prof) {
+            f();
+            return;
+        }
+        hipEvent_t a = get_event(), b = get_event();
+        HIPCHK(hipEventRecord(a, stream));
+        f();
+        HIPCHK(hipEventRecord(b, stream));
+        pending.push_back({name, a, b});
+        if (pending.size() > 4096) flush_timers();
+    }
+
+    void flush_timers() {
+        if (pending.empty()) return;
+        (void)hipStreamSynchronize(stream);
+        for (auto& p : pending) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+                timers[p.name].ms += ms;
+                timers[p.name].launches += 1;
+            }
+            event_pool.push_back(p.a);
+            event_pool.push_back(p.b);
+        }
+        pending.clear();
+    }
+};
+
+namespace {
+
+kb2e_status fail(kb2e_ctx* c, kb2e_status s, const std::string& msg) {
+    if (c) c->err = msg;
+    return s;
+}
+
+template <class F>
+kb2e_status guarded(kb2e_ctx* c, F&& f) {
+    if (!c) return KB2E_EINVAL;
+    try {
+        return f();
+    } catch (const HipError& e) {
+        return fail(c, KB2E_EDEVICE, e.what());
+    } catch (const std::invalid_argument& e) {
+        return fail(c, KB2E_EINVAL, e.what());
+    } catch (const std::bad_alloc&) {
+        return fail(c, KB2E_ENOMEM, "host out of memory");
+    } catch (const std::exception& e) {
+        return fail(c, KB2E_EDEVICE, e.what());
+    }
+}
+
+// ------------------------------------------------------------ table transfer
+
+template <typename T>
+void upload_rows(kb2e_ctx* c, DevBuf& dst, const double* src, int64_t rows, int n, int ld) {
+    std::vector<T> tmp((size_t)rows * ld, T(0));
+    for (int64_t r = 0; r < rows; ++r)
+        for (int i = 0; i < n; ++i) tmp[(size_t)r * ld + i] = (T)src[(size_t)r * n + i];
+    HIPCHK(hipMemcpyAsync(dst.p, tmp.data(), tmp.size() * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+}
+
+template <typename T>
+void download_rows(kb2e_ctx* c, const DevBuf& src, double* dst, int64_t rows, int n, int ld) {
+    std::vector<T> tmp((size_t)rows * ld);
+    HIPCHK(hipMemcpyAsync(tmp.data(), src.p, tmp.size() * sizeof(T), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int64_t r = 0; r < rows; ++r)
+        for (int i = 0; i < n; ++i) dst[(size_t)r * n + i] = (double)tmp[(size_t)r * ld + i];
+}
+
+int64_t w_rows(const kb2e_ctx* c) {
+    if (c->cfg.model == KB2E_TRANSH) return c->cfg.num_relations;
+    if (c->cfg.model == KB2E_TRANSR) return (int64_t)c->cfg.num_relations * c->n;
+    return 0;
+}
+
+void upload_tables(kb2e_ctx* c, const double* e, const double* r, const double* w) {
+    const int64_t ne = c->cfg.num_entities, nr = c->cfg.num_relations;
+    if (c->f64()) {
+        if (e) upload_rows<double>(c, c->ent, e, ne, c->n, c->ld);
+        if (r) upload_rows<double>(c, c->rel, r, nr, c->n, c->ld);
+        if (w && w_rows(c)) upload_rows<double>(c, c->w, w, w_rows(c), c->n, c->ld);
+    } else {
+        if (e) upload_rows<float>(c, c->ent, e, ne, c->n, c->ld);
+        if (r) upload_rows<float>(c, c->rel, r, nr, c->n, c->ld);
+        if (w && w_rows(c)) upload_rows<float>(c, c->w, w, w_rows(c), c->n, c->ld);
+    }
+}
+
+// ------------------------------------------------------------------- index
+
+void build_index(kb2e_ctx* c) {
+    const int64_t nkeys = c->S * c->slots;
+    KeyArgs ka{};
+    ka.heads = c->heads.as<int32_t>();
+    ka.tails = c->tails.as<int32_t>();
+    ka.rels = c->rels.as<int32_t>();
+    ka.si = c->si.as<int32_t>();
+    ka.sj = c->sj.as<int32_t>();
+    ka.side = c->side.as<uint8_t>();
+    ka.owner = c->cfg.model == KB2E_TRANSE ? nullptr : c->owner.as<int32_t>();
+    ka.nsamples = c->S;
+    ka.B = (int32_t)c->B;
+    ka.ne = c->cfg.num_entities;
+    ka.kl = c->kl;
+    ka.keys = c->keys.as<uint64_t>();
+    const int grid = (int)((c->S + 255) / 256);
+    c->timed("index", [&] {
+        if (c->cfg.model == KB2E_TRANSR)
+            emit_keys_kernel<8, true><<<grid, 256, 0, c->stream>>>(ka);
+        else
+            emit_keys_kernel<6, false><<<grid, 256, 0, c->stream>>>(ka);
+        HIPCHK(hipGetLastError());
+        size_t tb = c->sort_tmp_bytes;
+        HIPCHK(hipcub::DeviceRadixSort::SortKeys(c->sort_tmp.p, tb, c->keys.as<uint64_t>(),
+                                                 c->keys_sorted.as<uint64_t>(), (int)nkeys, 0,
+                                                 c->kl.total_bits(), c->stream));
+        const int g2 = (int)((nkeys + 255) / 256);
+        seg_flags_kernel<<<g2, 256, 0, c->stream>>>(c->keys_sorted.as<uint64_t>(), nkeys, c->kl,
+                                                     c->flags.as<int32_t>(), c->nvalid.as<int32_t>());
+        HIPCHK(hipGetLastError());
+        tb = c->sort_tmp_bytes;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, tb, c->flags.as<int32_t>(),
+                                                c->idx.as<int32_t>(), (int)nkeys, c->stream));
+        seg_scatter_kernel<<<g2, 256, 0, c->stream>>>(c->flags.as<int32_t>(), c->idx.as<int32_t>(), nkeys,
+                                                       c->seg_start.as<int32_t>(), c->nseg.as<int32_t>(),
+                                                       c->nvalid.as<int32_t>());
+        HIPCHK(hipGetLastError());
+        batch_begin_kernel<<<256, 256, 0, c->stream>>>(c->keys_sorted.as<uint64_t>(), c->seg_start.as<int32_t>(),
+                                                        c->nseg.as<int32_t>(), (int)c->nb, c->kl,
+                                                        c->batch_seg.as<int32_t>());
+        HIPCHK(hipGetLastError());
+    });
+}
+
+// ----------------------------------------------------------------- sampling
+
+void sample_epoch(kb2e_ctx* c) {
+    if (c->cfg.sampler == KB2E_SAMPLER_REPLAY) {
+        if (c->rp_pos + c->S > (int64_t)c->rp_si.size())
+            throw std::invalid_argument("replay stream exhausted: supply a full epoch of samples");
+        std::memcpy(c->pin_si, c->rp_si.data() + c->rp_pos, c->S * sizeof(int32_t));
+        std::memcpy(c->pin_sj, c->rp_sj.data() + c->rp_pos, c->S * sizeof(int32_t));
+        std::memcpy(c->pin_side, c->rp_side.data() + c->rp_pos, c->S);
+        c->rp_pos += c->S;
+    } else {
+        for (int64_t k = 0; k < c->S; ++k) {
+            if (!HostSampler::draw(c->rng, c->ts, c->cfg.method, c->pin_si[k], c->pin_sj[k], c->pin_side[k]))
+                throw std::runtime_error("negative sampler cannot terminate: every entity completes a training triple");
+        }
+    }
+    HIPCHK(hipMemcpyAsync(c->si.p, c->pin_si, c->S * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->sj.p, c->pin_sj, c->S * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->side.p, c->pin_side, c->S, hipMemcpyHostToDevice, c->stream));
+}
+
+// --------------------------------------------------------------- the batch
+
+template <typename T>
+ScoreArgs<T> score_args(kb2e_ctx* c, int64_t b) {
+    ScoreArgs<T> a{};
+    a.heads = c->heads.as<int32_t>();
+    a.tails = c->tails.as<int32_t>();
+    a.rels = c->rels.as<int32_t>();
+    a.si = c->si.as<int32_t>() + b * c->B;
+    a.sj = c->sj.as<int32_t>() + b * c->B;
+    a.side = c->side.as<uint8_t>() + b * c->B;
+    a.B = (int32_t)c->B;
+    a.n = c->n;
+    a.ld = c->ld;
+    a.nw = c->nw;
+    a.ent = c->ent.as<T>();
+    a.rel = c->rel.as<T>();
+    a.w = c->w.as<T>();
+    a.margin = c->cfg.margin;
+    a.act = c->act.as<uint8_t>() + b * c->B;
+    a.loss = c->loss.as<double>() + b * c->B;
+    a.xbits = c->xbits.as<uint64_t>();
+    a.xreal = c->xreal.as<T>();
+    return a;
+}
+
+template <typename T, int CH>
+void run_batch_transe(kb2e_ctx* c, int64_t b) {
+    ScoreArgs<T> sa = score_args<T>(c, b);
+    const bool l1 = c->cfg.distance == 0;
+    const int grid = (int)((c->B + 3) / 4);
+    c->timed("score", [&] {
+        if (l1) transe_score_kernel<T, CH, true><<<grid, 256, 0, c->stream>>>(sa);
+        else transe_score_kernel<T, CH, false><<<grid, 256, 0, c->stream>>>(sa);
+        HIPCHK(hipGetLastError());
+    });
+    FoldArgs<T> fa{};
+    fa.keys = c->keys_sorted.as<uint64_t>();
+    fa.seg_start = c->seg_start.as<int32_t>();
+    fa.batch_seg = c->batch_seg.as<int32_t>();
+    fa.batch = (int32_t)b;
+    fa.kl = c->kl;
+    fa.ne = c->cfg.num_entities;
+    fa.n = c->n;
+    fa.ld = c->ld;
+    fa.nw = c->nw;
+    fa.ent = c->ent.as<T>();
+    fa.rel = c->rel.as<T>();
+    fa.lr = c->cfg.learning_rate;
+    fa.act = sa.act;
+    fa.xbits = sa.xbits;
+    fa.xreal = sa.xreal;
+    // Enough waves for every touched row of a batch (<= 6 B segments).
+    const int64_t max_seg = std::min<int64_t>(c->B * 6, (int64_t)c->cfg.num_entities + c->cfg.num_relations);
+    const int fgrid = (int)std::max<int64_t>(1, std::min<int64_t>((max_seg + 3) / 4, 4096));
+    c->timed("fold", [&] {
+        if (l1) transe_fold_kernel<T, CH, true><<<fgrid, 256, 0, c->stream>>>(fa);
+        else transe_fold_kernel<T, CH, false><<<fgrid, 256, 0, c->stream>>>(fa);
+        HIPCHK(hipGetLastError());
+    });
+}
+
+template <typename T>
+void run_batch(kb2e_ctx* c, int64_t b) {
+    if (c->cfg.model == KB2E_TRANSE) {
+        switch (c->ch) {
+            case 1: run_batch_transe<T, 1>(c, b); break;
+            case 2: run_batch_transe<T, 2>(c, b); break;
+            default: run_batch_transe<T, 4>(c, b); break;
+        }
+    } else {
+        run_batch_relowner<T>(c, b);
+    }
+}
+
+__global__ void reduce_stats_kernel(const double* loss, const uint8_t* act, int64_t lo, int64_t hi, double* out) {
+    __shared__ double sl[1024];
+    __shared__ double sa[1024];
+    double l = 0, a = 0;
+    for (int64_t k = lo + threadIdx.x; k < hi; k += blockDim.x) {
+        l += loss[k];
+        a += act[k];
+    }
+    sl[threadIdx.x] = l;
+    sa[threadIdx.x] = a;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            sl[threadIdx.x] += sl[threadIdx.x + s];
+            sa[threadIdx.x] += sa[threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = sl[0];
+        out[1] = sa[0];
+    }
+}
+
+// Fold the stats of samples [reduced_upto, upto) of the current epoch into the
+// host accumulators (synchronises the stream).
+void reduce_stats(kb2e_ctx* c, int64_t upto) {
+    if (upto <= c->reduced_upto) return;
+    reduce_stats_kernel<<<1, 1024, 0, c->stream>>>(c->loss.as<double>(), c->act.as<uint8_t>(), c->reduced_upto,
+                                                   upto, c->stats.as<double>());
+    HIPCHK(hipGetLastError());
+    double h[2];
+    HIPCHK(hipMemcpyAsync(h, c->stats.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->acc_loss += h[0];
+    c->acc_active += (int64_t)llround(h[1]);
+    c->reduced_upto = upto;
+}
+
+void run_batches(kb2e_ctx* c, int64_t count) {
+    if (!c->have_triples || !c->have_params) throw std::logic_error("upload triples and params first");
+    for (int64_t q = 0; q < count; ++q) {
+        if (c->epoch_pos == 0 && !c->epoch_ready) {
+            sample_epoch(c);
+            build_index(c);
+            c->epoch_ready = true;
+            c->reduced_upto = 0;
+        }
+        if (c->f64()) run_batch<double>(c, c->epoch_pos);
+        else run_batch<float>(c, c->epoch_pos);
+        if (++c->epoch_pos == c->nb) {
+            reduce_stats(c, c->S);
+            c->epoch_pos = 0;
+            c->epoch_ready = false;
+        }
+    }
+}
+
+void setup_buffers(kb2e_ctx* c) {
+    const kb2e_config& g = c->cfg;
+    c->esize = c->f64() ? 8 : 4;
+    c->n = g.dim;
+    c->ld = (g.dim + 1) & ~1;
+    c->ch = (g.dim + kWave * kVec - 1) / (kWave * kVec);
+    c->nw = c->ch * kVec;
+    const size_t es = (size_t)c->esize;
+    c->ent.alloc((size_t)g.num_entities * c->ld * es);
+    c->rel.alloc((size_t)g.num_relations * c->ld * es);
+    HIPCHK(hipMemset(c->ent.p, 0, c->ent.bytes));
+    HIPCHK(hipMemset(c->rel.p, 0, c->rel.bytes));
+    if (g.model == KB2E_TRANSH) c->w_elems = (int64_t)g.num_relations * g.dim;
+    if (g.model == KB2E_TRANSR) c->w_elems = (int64_t)g.num_relations * g.dim * g.dim;
+    c->w.alloc((size_t)std::max<int64_t>(1, w_rows(c)) * c->ld * es);
+    HIPCHK(hipMemset(c->w.p, 0, c->w.bytes));
+    c->device_bytes = (int64_t)(c->ent.bytes + c->rel.bytes + c->w.bytes);
+}
+
+void setup_epoch_buffers(kb2e_ctx* c) {
+    const kb2e_config& g = c->cfg;
+    const int64_t ntrain = c->ts.size();
+    c->B = ntrain / g.num_batches;
+    c->nb = g.num_batches;
+    c->S = c->B * c->nb;
+    if (c->B < 1) throw std::invalid_argument("fewer training triples than batches");
+    c->si.alloc(c->S * 4);
+    c->sj.alloc(c->S * 4);
+    c->side.alloc(c->S);
+    if (c->pin_si) { (void)hipHostFree(c->pin_si); (void)hipHostFree(c->pin_sj); (void)hipHostFree(c->pin_side); }
+    HIPCHK(hipHostMalloc((void**)&c->pin_si, c->S * 4, 0));
+    HIPCHK(hipHostMalloc((void**)&c->pin_sj, c->S * 4, 0));
+    HIPCHK(hipHostMalloc((void**)&c->pin_side, c->S, 0));
+    // keys
+    c->slots = g.model == KB2E_TRANSR ? 8 : 6;
+    const int64_t nowners = g.model == KB2E_TRANSE ? g.num_relations : c->plan.num_owners;
+    c->kl.kk_bits = bits_for(c->B);
+    c->kl.row_bits = bits_for((int64_t)g.num_entities + nowners);
+    c->kl.batch_bits = bits_for(c->nb);  // holds nb, so batch nb-1 is never all-ones
+    if (c->kl.total_bits() > 64) throw std::invalid_argument("problem too large for 64-bit event keys");
+    const int64_t nkeys = c->S * c->slots;
+    if (nkeys >= (1ll << 31)) throw std::invalid_argument("epoch too large for one index (> 2^31 events)");
+    c->keys.alloc(nkeys * 8);
+    c->keys_sorted.alloc(nkeys * 8);
+    c->flags.alloc(nkeys * 4);
+    c->idx.alloc(nkeys * 4);
+    c->seg_start.alloc((nkeys + 1) * 4);
+    c->nseg.alloc(16);
+    c->nvalid.alloc(16);
+    c->batch_seg.alloc((c->nb + 1) * 4);
+    size_t t1 = 0, t2 = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, t1, (uint64_t*)nullptr, (uint64_t*)nullptr, (int)nkeys, 0,
+                                             c->kl.total_bits(), c->stream));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (int32_t*)nullptr, (int32_t*)nullptr, (int)nkeys,
+                                            c->stream));
+    c->sort_tmp_bytes = std::max(t1, t2);
+    c->sort_tmp.alloc(c->sort_tmp_bytes);
+    c->act.alloc(c->S);
+    c->loss.alloc(c->S * 8);
+    c->xbits.alloc((size_t)c->B * 2 * c->nw * 8);
+    if (g.distance != 0 || g.model == KB2E_TRANSR)
+        c->xreal.alloc((size_t)c->B * 2 * c->ld * c->esize);
+    c->stats.alloc(64);
+    setup_relowner_buffers(c);
+    c->device_bytes = 0;
+    for (DevBuf* d : {&c->ent, &c->rel, &c->w, &c->heads, &c->tails, &c->rels, &c->si, &c->sj, &c->side,
+                      &c->keys, &c->keys_sorted, &c->sort_tmp, &c->flags, &c->idx, &c->seg_start, &c->act,
+                      &c->loss, &c->xbits, &c->xreal, &c->aux, &c->tickets, &c->ent_done, &c->wsnap})
+        c->device_bytes += (int64_t)d->bytes;
+}
+
+}  // namespace
+
+#include "engine_relowner.inc"
+
+// ================================================================== C ABI
+
+extern "C" {
+
+void kb2e_default_config(kb2e_config* cfg) {
+    if (!cfg) return;
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->model = KB2E_TRANSE;
+    cfg->dim = 100;              // DEFAULT_EMBEDDING_SIZE
+    cfg->learning_rate = 0.001;  // DEFAULT_LEARNING_RATE
+    cfg->margin = 1.0;           // DEFAULT_MARGIN
+    cfg->method = 1;             // DEFAULT_METHOD = bern
+    cfg->distance = 0;           // DEFAULT_DISTANCE = L1
+    cfg->num_batches = 100;      // DEFAULT_NUM_BATCHES
+    cfg->seed = 0;
+    cfg->precision = 64;
+    cfg->sampler = KB2E_SAMPLER_GLIBC;
+    cfg->transr_compat = 1;
+    cfg->device = 0;
+}
+
+kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
+    if (!cfg || !out) return KB2E_EINVAL;
+    *out = nullptr;
+    const kb2e_config& g = *cfg;
+    if (g.model < 0 || g.model > 2 || g.dim < 1 || g.dim > 512 || g.num_entities < 1 || g.num_relations < 1 ||
+        g.num_batches < 1 || (g.precision != 32 && g.precision != 64) || (g.method != 0 && g.method != 1) ||
+        (g.distance != 0 && g.distance != 1) || (g.sampler != 0 && g.sampler != 1))
+        return KB2E_EINVAL;
+    if (g.model == KB2E_TRANSR && g.num_relations > g.num_entities) return KB2E_EINVAL;  // entityVec_next_[relation]
+    std::unique_ptr<kb2e_ctx> c(new kb2e_ctx());
+    c->cfg = g;
+    c->rng.seed_with(g.seed);
+    kb2e_status s = guarded(c.get(), [&] {
+        int ndev = 0;
+        HIPCHK(hipGetDeviceCount(&ndev));
+        if (g.device < 0 || g.device >= ndev) return fail(c.get(), KB2E_EDEVICE, "no such HIP device");
+        HIPCHK(hipSetDevice(g.device));
+        HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        setup_buffers(c.get());
+        return KB2E_OK;
+    });
+    if (s != KB2E_OK) return s;
+    *out = c.release();
+    return KB2E_OK;
+}
+
+void kb2e_destroy(kb2e_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->cfg.device);
+    delete ctx;
+}
+
+const char* kb2e_last_error(const kb2e_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+kb2e_status kb2e_upload_triples(kb2e_ctx* c, const int32_t* h, const int32_t* t, const int32_t* r, int64_t count) {
+    return guarded(c, [&] {
+        if (!h || !t || !r || count < 1) return fail(c, KB2E_EINVAL, "empty triple set");
+        HIPCHK(hipSetDevice(c->cfg.device));
+        c->ts.build(h, t, r, count, c->cfg.num_entities, c->cfg.num_relations);
+        c->heads.alloc(count * 4);
+        c->tails.alloc(count * 4);
+        c->rels.alloc(count * 4);
+        HIPCHK(hipMemcpy(c->heads.p, h, count * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(c->tails.p, t, count * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(c->rels.p, r, count * 4, hipMemcpyHostToDevice));
+        if (c->cfg.model != KB2E_TRANSE) plan_owners(c->plan, c->ts, c->cfg.num_relations);
+        setup_epoch_buffers(c);
+        c->have_triples = true;
+        c->epoch_pos = 0;
+        c->epoch_ready = false;
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_init_params(kb2e_ctx* c, double* ent_out, double* rel_out, double* w_out) {
+    return guarded(c, [&] {
+        HIPCHK(hipSetDevice(c->cfg.device));
+        const int n = c->n;
+        const int64_t ne = c->cfg.num_entities, nr = c->cfg.num_relations;
+        std::vector<double> E((size_t)ne * n), R((size_t)nr * n), W((size_t)std::max<int64_t>(c->w_elems, 1));
+        // initialEmbeddingValue: transe/trainer.cpp:21-23, transh/trainer.cpp:61-63, transr/trainer.cpp:66-68
+        auto init = [&]() {
+            if (c->cfg.model == KB2E_TRANSE)
+                return randn(c->rng, 0, 1.0 / n, -6 / std::sqrt((double)n), 6 / std::sqrt((double)n));
+            return randn(c->rng, 0, 1.0 / n, -1, 1);
+        };
+        auto norm_row = [&](double* a, bool ignore_short) {  // common/utils.cpp:70-77
+            double res = 0;
+            for (int i = 0; i < n; ++i) res += a[i] * a[i];
+            double len = std::sqrt(res);
+            if (!ignore_short || len > 1)
+                for (int i = 0; i < n; ++i) a[i] /= len;
+        };
+        // common/trainer.cpp:45-57: relations first, then entities.
+        for (int64_t i = 0; i < nr; ++i) {
+            for (int j = 0; j < n; ++j) R[(size_t)i * n + j] = init();
+            norm_row(&R[(size_t)i * n], true);
+        }
+        for (int64_t i = 0; i < ne; ++i) {
+            for (int j = 0; j < n; ++j) E[(size_t)i * n + j] = init();
+            norm_row(&E[(size_t)i * n], true);
+        }
+        if (c->cfg.model == KB2E_TRANSH) {  // transh/trainer.cpp:80-87
+            for (int64_t i = 0; i < nr; ++i) {
+                for (int j = 0; j < n; ++j) W[(size_t)i * n + j] = init();
+                norm_row(&W[(size_t)i * n], false);
+            }
+        } else if (c->cfg.model == KB2E_TRANSR) {  // transr/trainer.cpp:73-86: identity
+            for (int64_t i = 0; i < nr; ++i)
+                for (int j = 0; j < n; ++j)
+                    for (int k = 0; k < n; ++k) W[((size_t)i * n + j) * n + k] = (j == k) ? 1.0 : 0.0;
+        }
+        upload_tables(c, E.data(), R.data(), c->w_elems ? W.data() : nullptr);
+        if (ent_out) std::memcpy(ent_out, E.data(), E.size() * 8);
+        if (rel_out) std::memcpy(rel_out, R.data(), R.size() * 8);
+        if (w_out && c->w_elems) std::memcpy(w_out, W.data(), (size_t)c->w_elems * 8);
+        c->have_params = true;
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_upload_params(kb2e_ctx* c, const double* e, const double* r, const double* w) {
+    return guarded(c, [&] {
+        HIPCHK(hipSetDevice(c->cfg.device));
+        if (!e || !r || (c->w_elems && !w && !c->have_params))
+            return fail(c, KB2E_EINVAL, "entity, relation (and weight) tables required");
+        upload_tables(c, e, r, w);
+        c->have_params = true;
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_download_params(kb2e_ctx* c, double* e, double* r, double* w) {
+    return guarded(c, [&] {
+        HIPCHK(hipSetDevice(c->cfg.device));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        const int64_t ne = c->cfg.num_entities, nr = c->cfg.num_relations;
+        if (c->f64()) {
+            if (e) download_rows<double>(c, c->ent, e, ne, c->n, c->ld);
+            if (r) download_rows<double>(c, c->rel, r, nr, c->n, c->ld);
+            if (w && w_rows(c)) download_rows<double>(c, c->w, w, w_rows(c), c->n, c->ld);
+        } else {
+            if (e) download_rows<float>(c, c->ent, e, ne, c->n, c->ld);
+            if (r) download_rows<float>(c, c->rel, r, nr, c->n, c->ld);
+            if (w && w_rows(c)) download_rows<float>(c, c->w, w, w_rows(c), c->n, c->ld);
+        }
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_get_transr_work(kb2e_ctx* c, double* hw, double* tw) {
+    return guarded(c, [&] {
+        if (c->cfg.model != KB2E_TRANSR) return fail(c, KB2E_EUNSUPPORTED, "TransR only");
+        HIPCHK(hipStreamSynchronize(c->stream));
+        std::vector<double> h(2 * (size_t)c->n);
+        HIPCHK(hipMemcpy(h.data(), c->transr_work.p, h.size() * 8, hipMemcpyDeviceToHost));
+        std::memcpy(hw, h.data(), (size_t)c->n * 8);
+        std::memcpy(tw, h.data() + c->n, (size_t)c->n * 8);
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_set_transr_work(kb2e_ctx* c, const double* hw, const double* tw) {
+    return guarded(c, [&] {
+        if (c->cfg.model != KB2E_TRANSR) return fail(c, KB2E_EUNSUPPORTED, "TransR only");
+        if (!c->have_triples) return fail(c, KB2E_ESTATE, "upload triples first");
+        std::vector<double> h(2 * (size_t)c->n);
+        std::memcpy(h.data(), hw, (size_t)c->n * 8);
+        std::memcpy(h.data() + c->n, tw, (size_t)c->n * 8);
+        HIPCHK(hipMemcpy(c->transr_work.p, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_set_sample_stream(kb2e_ctx* c, const int32_t* i, const int32_t* j, const uint8_t* side,
+                                   int64_t count) {
+    return guarded(c, [&] {
+        if (!c->have_triples) return fail(c, KB2E_ESTATE, "upload triples first");
+        for (int64_t k = 0; k < count; ++k)
+            if (i[k] < 0 || i[k] >= c->ts.size() || j[k] < 0 || j[k] >= c->cfg.num_entities)
+                return fail(c, KB2E_EINVAL, "sample " + std::to_string(k) + " out of range");
+        c->rp_si.assign(i, i + count);
+        c->rp_sj.assign(j, j + count);
+        c->rp_side.assign(side, side + count);
+        c->rp_pos = 0;
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_train_batches(kb2e_ctx* c, int32_t nbatches) {
+    return guarded(c, [&] {
+        if (!c->have_triples || !c->have_params) return fail(c, KB2E_ESTATE, "upload triples and params first");
+        HIPCHK(hipSetDevice(c->cfg.device));
+        run_batches(c, nbatches);
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_synchronize(kb2e_ctx* c) {
+    return guarded(c, [&] {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
+    return guarded(c, [&] {
+        if (c->have_triples) reduce_stats(c, c->epoch_pos * c->B);
+        if (loss) *loss = c->acc_loss;
+        if (active) *active = c->acc_active;
+        c->acc_loss = 0;
+        c->acc_active = 0;
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_train_epoch(kb2e_ctx* c, double* loss, int64_t* active) {
+    return guarded(c, [&] {
+        if (!c->have_triples || !c->have_params) return fail(c, KB2E_ESTATE, "upload triples and params first");
+        if (c->epoch_pos != 0) return fail(c, KB2E_ESTATE, "an epoch is partially trained (kb2e_train_batches)");
+        HIPCHK(hipSetDevice(c->cfg.device));
+        c->acc_loss = 0;
+        c->acc_active = 0;
+        run_batches(c, c->nb);
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (loss) *loss = c->acc_loss;
+        if (active) *active = c->acc_active;
+        c->acc_loss = 0;
+        c->acc_active = 0;
+        return KB2E_OK;
+    });
+}
+
+int32_t kb2e_rng_next(kb2e_ctx* c) { return c ? c->rng.next() : -1; }
+
+kb2e_status kb2e_profile_enable(kb2e_ctx* c, int32_t on) {
+    return guarded(c, [&] {
+        c->flush_timers();
+        c->prof = on != 0;
+        c->timers.clear();
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_profile_query(kb2e_ctx* c, const char* name, double* total_ms, int64_t* launches) {
+    return guarded(c, [&] {
+        c->flush_timers();
+        auto it = c->timers.find(name ? name : "");
+        if (total_ms) *total_ms = it == c->timers.end() ? 0.0 : it->second.ms;
+        if (launches) *launches = it == c->timers.end() ? 0 : it->second.launches;
+        return KB2E_OK;
+    });
+}
+
+int64_t kb2e_device_bytes(const kb2e_ctx* c) { return c ? c->device_bytes : 0; }
+
+kb2e_status kb2e_device_tables(kb2e_ctx* c, void** e, void** r, void** w, int64_t* ne, int64_t* nr, int64_t* nw) {
+    return guarded(c, [&] {
+        if (e) *e = c->ent.p;
+        if (r) *r = c->rel.p;
+        if (w) *w = c->w_elems ? c->w.p : nullptr;
+        if (ne) *ne = (int64_t)c->cfg.num_entities * c->ld;
+        if (nr) *nr = (int64_t)c->cfg.num_relations * c->ld;
+        if (nw) *nw = c->w_elems ? w_rows(c) * c->ld : 0;
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_renormalize(kb2e_ctx* c) {
+    return guarded(c, [&] { return fail(c, KB2E_EUNSUPPORTED, "renormalize: not yet implemented"); });
+}
+
+}  // extern "C"

@@ -1,0 +1,125 @@
+// kernels_common.hpp -- shared device helpers for the kb2e_amd engine (gfx950).
+//
+// Row layout in HBM: every table is row-major with a leading dimension `ld`
+// (elements) rounded up to a multiple of 2, 16-byte aligned for FP64 pairs.
+// One 64-lane wave owns one row: lane l holds elements {128 c + 2 l, +1} for
+// chunks c < CH (CH = ceil(n / 128)).  Padding elements are zero and are never
+// written.  Reductions are deterministic xor-butterflies over the 64 lanes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace kb2e {
+
+constexpr int kWave = 64;
+constexpr int kVec = 2;  // elements per lane per chunk
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Read a wave-uniform 64-bit value held by lane `src` (src wave-uniform).
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int src) {
+    uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, src);
+    uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ int readlane_i32(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
+
+template <typename T, int CH>
+struct RowReg {
+    T v[CH][kVec];
+
+    __device__ __forceinline__ void load(const T* __restrict__ row, int n) {
+        const int l = lane_id();
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int e = c * (kWave * kVec) + l * kVec;
+            if (e < n) {
+                // ld is a multiple of 2, so the pair stays inside the row.
+                v[c][0] = row[e];
+                v[c][1] = row[e + 1];
+            } else {
+                v[c][0] = T(0);
+                v[c][1] = T(0);
+            }
+        }
+    }
+
+    __device__ __forceinline__ void store(T* __restrict__ row, int n) const {
+        const int l = lane_id();
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int e = c * (kWave * kVec) + l * kVec;
+            if (e < n) row[e] = v[c][0];
+            if (e + 1 < n) row[e + 1] = v[c][1];
+        }
+    }
+
+    // sum of squares over the wave (common/utils.cpp:44-51 computes it serially)
+    __device__ __forceinline__ T sumsq() const {
+        T s = T(0);
+#pragma unroll
+        for (int c = 0; c < CH; ++c) s += v[c][0] * v[c][0] + v[c][1] * v[c][1];
+        return wave_sum(s);
+    }
+
+    // common::norm (common/utils.cpp:70-77): scale to unit length if
+    // !ignoreShort or the length exceeds 1.  Division, as the reference.
+    __device__ __forceinline__ void norm(int n, bool ignore_short) {
+        const T len = sqrt(sumsq());
+        if (!ignore_short || len > T(1)) {
+            const int l = lane_id();
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                const int e = c * (kWave * kVec) + l * kVec;
+                if (e < n) v[c][0] = v[c][0] / len;
+                if (e + 1 < n) v[c][1] = v[c][1] / len;
+            }
+        }
+    }
+};
+
+// Is element (c, k) of this lane inside the row?
+__device__ __forceinline__ bool elem_valid(int c, int k, int n) {
+    return c * (kWave * kVec) + lane_id() * kVec + k < n;
+}
+
+// Sign bits of an update direction x: word (c * 2 + k) holds, at bit l, the
+// sign (x > 0) of element 128 c + 2 l + k.
+__device__ __forceinline__ bool xbit(const uint64_t* words, int c, int k) {
+    return (words[c * kVec + k] >> lane_id()) & 1ull;
+}
+
+// ---- event keys: [batch | row | kk | u | roles] (most to least significant)
+struct KeyLayout {
+    int kk_bits, row_bits, batch_bits;
+    __host__ __device__ int kk_shift() const { return 4; }
+    __host__ __device__ int row_shift() const { return 4 + kk_bits; }
+    __host__ __device__ int batch_shift() const { return 4 + kk_bits + row_bits; }
+    __host__ __device__ int total_bits() const { return 4 + kk_bits + row_bits + batch_bits; }
+    __host__ __device__ uint64_t make(uint64_t batch, uint64_t row, uint64_t kk, uint64_t u,
+                                      uint64_t roles) const {
+        return (batch << batch_shift()) | (row << row_shift()) | (kk << kk_shift()) | (u << 3) | roles;
+    }
+    __host__ __device__ uint64_t seg_part(uint64_t key) const { return key >> row_shift(); }
+    __host__ __device__ int batch_of(uint64_t key) const { return (int)(key >> batch_shift()); }
+    __host__ __device__ int row_of(uint64_t key) const {
+        return (int)((key >> row_shift()) & ((1ull << row_bits) - 1));
+    }
+    __host__ __device__ int kk_of(uint64_t key) const {
+        return (int)((key >> kk_shift()) & ((1ull << kk_bits) - 1));
+    }
+};
+
+constexpr uint64_t kSentinelKey = ~0ull;
+enum : uint32_t { kRoleHead = 1, kRoleTail = 2, kRoleEntRel = 4 };
+
+}  // namespace kb2e

@@ -1,0 +1,207 @@
+"""ctypes binding of libkb2e.so (include/kb2e_engine.h).
+
+This is the product path for Python callers (bench.py, tests): every call goes
+through the C ABI into the HIP engine.  There is no CPU fallback -- if the
+library or a GPU is missing, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libkb2e.so")
+
+MODELS = {"transe": 0, "transh": 1, "transr": 2, "E": 0, "H": 1, "R": 2}
+STATUS = {0: "OK", 1: "EINVAL", 2: "EDEVICE", 3: "ESTATE", 4: "ENOMEM", 5: "EUNSUPPORTED", 6: "ESAMPLER"}
+SAMPLER_GLIBC, SAMPLER_REPLAY = 0, 1
+
+# Every symbol include/kb2e_engine.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "kb2e_default_config", "kb2e_create", "kb2e_destroy", "kb2e_last_error", "kb2e_upload_triples",
+    "kb2e_init_params", "kb2e_upload_params", "kb2e_download_params", "kb2e_get_transr_work",
+    "kb2e_set_transr_work", "kb2e_set_sample_stream", "kb2e_train_epoch", "kb2e_train_batches",
+    "kb2e_synchronize", "kb2e_take_stats", "kb2e_rng_next", "kb2e_profile_enable", "kb2e_profile_query",
+    "kb2e_device_bytes", "kb2e_device_tables", "kb2e_renormalize",
+]
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("model", C.c_int32), ("dim", C.c_int32), ("num_entities", C.c_int32), ("num_relations", C.c_int32),
+        ("learning_rate", C.c_double), ("margin", C.c_double), ("method", C.c_int32), ("distance", C.c_int32),
+        ("num_batches", C.c_int32), ("seed", C.c_uint32), ("precision", C.c_int32), ("sampler", C.c_int32),
+        ("transr_compat", C.c_int32), ("device", C.c_int32),
+    ]
+
+
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"kb2e HIP engine not built: {LIB_PATH} missing (run `make`)")
+        L = C.CDLL(LIB_PATH)
+        vp, i32, i64, dp = C.c_void_p, C.c_int32, C.c_int64, C.POINTER(C.c_double)
+        i32p, u8p = C.POINTER(C.c_int32), C.POINTER(C.c_uint8)
+        sig = {
+            "kb2e_default_config": (None, [C.POINTER(Config)]),
+            "kb2e_create": (i32, [C.POINTER(Config), C.POINTER(vp)]),
+            "kb2e_destroy": (None, [vp]),
+            "kb2e_last_error": (C.c_char_p, [vp]),
+            "kb2e_upload_triples": (i32, [vp, i32p, i32p, i32p, i64]),
+            "kb2e_init_params": (i32, [vp, dp, dp, dp]),
+            "kb2e_upload_params": (i32, [vp, dp, dp, dp]),
+            "kb2e_download_params": (i32, [vp, dp, dp, dp]),
+            "kb2e_get_transr_work": (i32, [vp, dp, dp]),
+            "kb2e_set_transr_work": (i32, [vp, dp, dp]),
+            "kb2e_set_sample_stream": (i32, [vp, i32p, i32p, u8p, i64]),
+            "kb2e_train_epoch": (i32, [vp, dp, C.POINTER(i64)]),
+            "kb2e_train_batches": (i32, [vp, i32]),
+            "kb2e_synchronize": (i32, [vp]),
+            "kb2e_take_stats": (i32, [vp, dp, C.POINTER(i64)]),
+            "kb2e_rng_next": (i32, [vp]),
+            "kb2e_profile_enable": (i32, [vp, i32]),
+            "kb2e_profile_query": (i32, [vp, C.c_char_p, dp, C.POINTER(i64)]),
+            "kb2e_device_bytes": (i64, [vp]),
+            "kb2e_device_tables": (i32, [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(i64),
+                                         C.POINTER(i64), C.POINTER(i64)]),
+            "kb2e_renormalize": (i32, [vp]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def _dp(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _ip(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+class Engine:
+    """One training context on one GPU (the drop-in for Trainer::bfgs)."""
+
+    def __init__(self, model, dim, num_entities, num_relations, *, rate=0.001, margin=1.0, method=1,
+                 distance=0, batches=100, seed=0, precision=64, sampler=SAMPLER_GLIBC, transr_compat=True,
+                 device=0):
+        self.kind = MODELS[model] if isinstance(model, str) else int(model)
+        self.n, self.ne, self.nr = dim, num_entities, num_relations
+        cfg = Config()
+        lib().kb2e_default_config(C.byref(cfg))
+        cfg.model, cfg.dim, cfg.num_entities, cfg.num_relations = self.kind, dim, num_entities, num_relations
+        cfg.learning_rate, cfg.margin, cfg.method, cfg.distance = rate, margin, method, distance
+        cfg.num_batches, cfg.seed, cfg.precision, cfg.sampler = batches, seed, precision, sampler
+        cfg.transr_compat, cfg.device = int(transr_compat), device
+        self.cfg = cfg
+        h = C.c_void_p()
+        st = lib().kb2e_create(C.byref(cfg), C.byref(h))
+        if st != 0:
+            raise EngineError(f"kb2e_create failed: {STATUS.get(st, st)}")
+        self.h = h
+
+    def _check(self, st, what):
+        if st != 0:
+            msg = lib().kb2e_last_error(self.h)
+            raise EngineError(f"{what}: {STATUS.get(st, st)}: {msg.decode() if msg else ''}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().kb2e_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def wshape(self):
+        return {0: None, 1: (self.nr, self.n), 2: (self.nr, self.n, self.n)}[self.kind]
+
+    def upload_triples(self, triples):
+        t = np.ascontiguousarray(triples, dtype=np.int32)
+        cols = [np.ascontiguousarray(t[:, k]) for k in range(3)]
+        self._check(lib().kb2e_upload_triples(self.h, _ip(cols[0]), _ip(cols[1]), _ip(cols[2]), len(t)),
+                    "upload_triples")
+
+    def init_params(self):
+        ent = np.zeros((self.ne, self.n))
+        rel = np.zeros((self.nr, self.n))
+        w = np.zeros(self.wshape()) if self.wshape() else None
+        self._check(lib().kb2e_init_params(self.h, _dp(ent), _dp(rel), _dp(w)), "init_params")
+        return ent, rel, w
+
+    def upload_params(self, ent, rel, w=None):
+        ent = np.ascontiguousarray(ent, dtype=np.float64)
+        rel = np.ascontiguousarray(rel, dtype=np.float64)
+        w = None if w is None else np.ascontiguousarray(w, dtype=np.float64)
+        self._check(lib().kb2e_upload_params(self.h, _dp(ent), _dp(rel), _dp(w)), "upload_params")
+
+    def download_params(self):
+        ent = np.zeros((self.ne, self.n))
+        rel = np.zeros((self.nr, self.n))
+        w = np.zeros(self.wshape()) if self.wshape() else None
+        self._check(lib().kb2e_download_params(self.h, _dp(ent), _dp(rel), _dp(w)), "download_params")
+        return ent, rel, w
+
+    def transr_work(self):
+        a, b = np.zeros(self.n), np.zeros(self.n)
+        self._check(lib().kb2e_get_transr_work(self.h, _dp(a), _dp(b)), "get_transr_work")
+        return a, b
+
+    def set_transr_work(self, a, b):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        self._check(lib().kb2e_set_transr_work(self.h, _dp(a), _dp(b)), "set_transr_work")
+
+    def set_sample_stream(self, si, sj, side):
+        si = np.ascontiguousarray(si, dtype=np.int32)
+        sj = np.ascontiguousarray(sj, dtype=np.int32)
+        side = np.ascontiguousarray(side, dtype=np.uint8)
+        self._keep = (si, sj, side)
+        self._check(lib().kb2e_set_sample_stream(self.h, _ip(si), _ip(sj),
+                                                 side.ctypes.data_as(C.POINTER(C.c_uint8)), len(si)),
+                    "set_sample_stream")
+
+    def train_epoch(self):
+        loss = C.c_double(0)
+        act = C.c_int64(0)
+        self._check(lib().kb2e_train_epoch(self.h, C.byref(loss), C.byref(act)), "train_epoch")
+        return loss.value, act.value
+
+    def train_batches(self, nb):
+        self._check(lib().kb2e_train_batches(self.h, int(nb)), "train_batches")
+
+    def synchronize(self):
+        self._check(lib().kb2e_synchronize(self.h), "synchronize")
+
+    def take_stats(self):
+        loss = C.c_double(0)
+        act = C.c_int64(0)
+        self._check(lib().kb2e_take_stats(self.h, C.byref(loss), C.byref(act)), "take_stats")
+        return loss.value, act.value
+
+    def rng_next(self):
+        return lib().kb2e_rng_next(self.h)
+
+    def profile(self, on=True):
+        self._check(lib().kb2e_profile_enable(self.h, int(on)), "profile_enable")
+
+    def profile_query(self, name):
+        ms = C.c_double(0)
+        n = C.c_int64(0)
+        self._check(lib().kb2e_profile_query(self.h, name.encode(), C.byref(ms), C.byref(n)), "profile_query")
+        return ms.value, n.value
+
+    def device_bytes(self):
+        return lib().kb2e_device_bytes(self.h)

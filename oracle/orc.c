@@ -34,6 +34,8 @@ struct orc_model {
 };
 
 static long long g_orth_iters = 0;
+static long long g_site_iters[4];
+static int g_site = 3;
 static long long g_transr_norm_iters = 0;
 
 /* ------------------------------------------------------------------ L0 */
@@ -100,6 +102,7 @@ void orc_norm_orth(double* a, double* b, int n, double rate) {
         for (int i = 0; i < n; i++) x += b[i] * a[i];
         if (x > 0.1) {
             g_orth_iters++;
+            g_site_iters[g_site]++;
             for (int i = 0; i < n; i++) {
                 a[i] -= rate * b[i];
                 b[i] -= rate * a[i];
@@ -112,6 +115,9 @@ void orc_norm_orth(double* a, double* b, int n, double rate) {
 }
 
 long long orc_norm_orth_iterations(void) { return g_orth_iters; }
+/* instrumentation: coupling-loop iterations per call site (0 = relation / head,
+ * 1 = head / tail, 2 = tail / entity[relation], 3 = direct calls) */
+long long orc_site_iterations(int site) { return (site >= 0 && site < 4) ? g_site_iters[site] : 0; }
 
 /* transr/trainer.cpp:35-64; b is n x n with b[j*n+i] = weights[j][i]. */
 void orc_transr_norm(double* a, double* b, int n, double rate) {
@@ -124,6 +130,7 @@ void orc_transr_norm(double* a, double* b, int n, double rate) {
         }
         if (x <= 1) break;
         g_transr_norm_iters++;
+        g_site_iters[g_site]++;
         double lambda = 1;
         for (int i = 0; i < n; i++) {
             double tmp = 0;
@@ -448,9 +455,10 @@ static void transh_update(orc_model* m, int h, int t, int r, int corrupted) {
     orc_norm(nh, n, 1);
     orc_norm(nt, n, 1);
     orc_norm(nw, n, 0);
-    orc_norm_orth(nr_, nw, n, m->lr);
-    orc_norm_orth(nh, nw, n, m->lr);
-    orc_norm_orth(nt, nw, n, m->lr);
+    g_site = 0; orc_norm_orth(nr_, nw, n, m->lr);
+    g_site = 1; orc_norm_orth(nh, nw, n, m->lr);
+    g_site = 2; orc_norm_orth(nt, nw, n, m->lr);
+    g_site = 3;
 }
 
 /* transr/trainer.cpp:144-188 */
@@ -480,9 +488,10 @@ static void transr_update(orc_model* m, int h, int t, int r, int corrupted) {
     orc_norm(nh, n, 0);
     orc_norm(nt, n, 0);
     for (int i = 0; i < n; i++) orc_norm(Wn + (size_t)i * n, n, 0);
-    orc_transr_norm(nh, Wn, n, m->lr);
-    orc_transr_norm(nt, Wn, n, m->lr);
-    orc_transr_norm(ROW(m->ent_next, r), Wn, n, m->lr); /* transr/trainer.cpp:187 (sic) */
+    g_site = 0; orc_transr_norm(nh, Wn, n, m->lr);
+    g_site = 1; orc_transr_norm(nt, Wn, n, m->lr);
+    g_site = 2; orc_transr_norm(ROW(m->ent_next, r), Wn, n, m->lr); /* transr/trainer.cpp:187 (sic) */
+    g_site = 3;
 }
 
 void orc_gradient_update(orc_model* m, int h, int t, int r, int corrupted) {

@@ -40,6 +40,7 @@ double orc_vec_len(const double* a, int n);                      /* utils.cpp:44
 void orc_norm(double* a, int n, int ignore_short);               /* utils.cpp:70-77 */
 void orc_norm_orth(double* a, double* b, int n, double rate);    /* utils.cpp:79-111 */
 long long orc_norm_orth_iterations(void); /* instrumentation: loop iterations that modified a,b */
+long long orc_site_iterations(int site);
 
 /* ---- model lifecycle (common/trainer.{h,cpp}) ---- */
 orc_model* orc_create(int model, int dim, int num_entities, int num_relations,

@@ -38,6 +38,7 @@ def lib():
             "orc_norm_orth_iterations": (ll, []),
             "orc_transr_norm": (None, [dp, dp, C.c_int, C.c_double]),
             "orc_transr_norm_iterations": (ll, []),
+            "orc_site_iterations": (ll, [C.c_int]),
             "orc_create": (vp, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
                                 C.c_int, C.c_int, C.c_int, C.c_int]),
             "orc_destroy": (None, [vp]),

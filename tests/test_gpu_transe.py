@@ -1,0 +1,139 @@
+"""TransE on the GPU vs the reference (golden fixtures) and the C oracle.
+
+Parity bar (stated per test): FP64 engine within 1e-11 absolute of the FP64
+reference tables after every epoch, identical hinge-active counts, identical
+RNG consumption; FP32 engine within 2e-4 after one epoch.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from gpu_common import F32_ATOL, F64_ATOL, golden_engine, max_abs, oracle_model, tiny
+from kb2e_amd import data
+from kb2e_amd.engine import SAMPLER_GLIBC, SAMPLER_REPLAY, Engine
+from oracle import orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["transe_l1_bern", "transe_l2_unif"])
+def test_init_params_bit_exact(name):
+    eng, run, ds, (ent, rel, _) = golden_engine(name)
+    d = os.path.join(GOLDEN, name)
+    assert np.array_equal(ent, np.load(os.path.join(d, "init_ent.npy")))
+    assert np.array_equal(rel, np.load(os.path.join(d, "init_rel.npy")))
+    # the uploaded FP64 tables round-trip exactly
+    e2, r2, _ = eng.download_params()
+    assert np.array_equal(e2, ent) and np.array_equal(r2, rel)
+
+
+@pytest.mark.parametrize("name", ["transe_l1_bern", "transe_l2_unif"])
+def test_golden_training_run_fp64(name):
+    eng, run, ds, _ = golden_engine(name)
+    d = os.path.join(GOLDEN, name)
+    losses = np.load(os.path.join(d, "epoch_loss.npy"))
+    actives = np.load(os.path.join(d, "epoch_active.npy"))
+    for ep in range(run["flags"]["epochs"]):
+        loss, act = eng.train_epoch()
+        assert act == actives[ep]
+        assert abs(loss - losses[ep]) <= 1e-9 * max(1.0, abs(losses[ep]))
+        e, r, _ = eng.download_params()
+        assert max_abs(e, np.load(os.path.join(d, f"epoch{ep}_ent.npy"))) < F64_ATOL
+        assert max_abs(r, np.load(os.path.join(d, f"epoch{ep}_rel.npy"))) < F64_ATOL
+    # the engine consumed exactly the reference's number of rand() calls
+    after = np.load(os.path.join(d, "rand_after.npy"))
+    assert [eng.rng_next() for _ in range(after.size)] == after.tolist()
+
+
+def test_golden_training_run_fp32():
+    eng, run, ds, _ = golden_engine("transe_l1_bern", precision=32)
+    d = os.path.join(GOLDEN, "transe_l1_bern")
+    loss, act = eng.train_epoch()
+    e, r, _ = eng.download_params()
+    assert max_abs(e, np.load(os.path.join(d, "epoch0_ent.npy"))) < F32_ATOL
+    assert max_abs(r, np.load(os.path.join(d, "epoch0_rel.npy"))) < F32_ATOL
+    assert abs(act - np.load(os.path.join(d, "epoch_active.npy"))[0]) <= 3
+
+
+def _oracle_vs_engine(ds, dim, epochs, *, distance=0, method=1, batches=20, rate=0.01, seed=3, atol=F64_ATOL):
+    m = oracle_model("E", ds, dim, rate=rate, margin=1.0, method=method, distance=distance, batches=batches)
+    orc.srand(seed)
+    m.prep_train()
+    eng = Engine("E", dim, ds.num_entities, ds.num_relations, rate=rate, margin=1.0, method=method,
+                 distance=distance, batches=batches, seed=seed)
+    eng.upload_triples(ds.train)
+    e0, r0, _ = eng.init_params()
+    oe, orl, _ = m.tables()
+    assert np.array_equal(e0, oe) and np.array_equal(r0, orl)
+    for ep in range(epochs):
+        lo, ao = m.train_epoch()
+        lg, ag = eng.train_epoch()
+        assert ag == ao, (ep, ag, ao)
+        assert abs(lg - lo) <= 1e-9 * max(1.0, abs(lo))
+        ge, gr, _ = eng.download_params()
+        oe, orl, _ = m.tables()
+        assert max_abs(ge, oe) < atol and max_abs(gr, orl) < atol, (ep, max_abs(ge, oe), max_abs(gr, orl))
+
+
+@pytest.mark.parametrize("dim,distance", [(50, 0), (100, 0), (100, 1), (17, 0), (200, 0), (130, 1)])
+def test_oracle_parity_small(dim, distance):
+    """Ragged and multi-chunk row widths (17, 130, 200) on a 30k-triple set."""
+    ds = data.synthetic("small", seed=1)
+    _oracle_vs_engine(ds, dim, 2, distance=distance)
+
+
+def test_single_batch_and_duplicates():
+    """batches=1 (one batch = the whole set) and duplicated / self-loop triples."""
+    ds = data.synthetic("tiny", seed=5)
+    extra = np.array([[3, 3, 1], [7, 7, 2]] + ds.train[:50].tolist(), dtype=np.int32)
+    ds.train = np.concatenate([ds.train, extra])
+    _oracle_vs_engine(ds, 20, 3, batches=1, method=0)
+
+
+def test_replay_stream_matches_oracle_replay():
+    ds = tiny()
+    m = oracle_model("E", ds, 20, rate=0.01, batches=10)
+    orc.srand(9)
+    m.prep_train()
+    e0, r0, _ = m.tables()
+    si, sj, side = m.sample_stream(3000)
+    eng = Engine("E", 20, ds.num_entities, ds.num_relations, rate=0.01, batches=10, sampler=SAMPLER_REPLAY)
+    eng.upload_triples(ds.train)
+    eng.upload_params(e0, r0)
+    eng.set_sample_stream(si, sj, side)
+    m.set_tables(e0, r0)
+    lo, ao = m.train_replay(si, sj, side)
+    lg, ag = eng.train_epoch()
+    ge, gr, _ = eng.download_params()
+    oe, orl, _ = m.tables()
+    assert ag == ao and max_abs(ge, oe) < F64_ATOL and max_abs(gr, orl) < F64_ATOL
+
+
+def test_train_batches_equals_train_epoch():
+    ds = tiny()
+    a = Engine("E", 20, ds.num_entities, ds.num_relations, rate=0.01, batches=10, seed=4)
+    b = Engine("E", 20, ds.num_entities, ds.num_relations, rate=0.01, batches=10, seed=4)
+    for e in (a, b):
+        e.upload_triples(ds.train)
+        e.init_params()
+    la, aa = a.train_epoch()
+    for _ in range(10):
+        b.train_batches(1)
+    lb, ab = b.take_stats()
+    assert aa == ab and abs(la - lb) < 1e-9
+    ea, ra, _ = a.download_params()
+    eb, rb, _ = b.download_params()
+    assert np.array_equal(ea, eb) and np.array_equal(ra, rb)
+
+
+def test_errors_are_loud():
+    ds = tiny()
+    eng = Engine("E", 20, ds.num_entities, ds.num_relations, batches=10)
+    with pytest.raises(Exception):
+        eng.train_epoch()  # no triples / params yet
+    bad = ds.train.copy()
+    bad[0, 0] = ds.num_entities + 5
+    with pytest.raises(Exception):
+        eng.upload_triples(bad)
