@@ -137,7 +137,14 @@ int64_t kb2e_device_bytes(const kb2e_ctx* ctx);
  * the reference's norm constraints after a merge. */
 kb2e_status kb2e_device_tables(kb2e_ctx* ctx, void** entity, void** relation, void** weights,
                                int64_t* n_entity, int64_t* n_relation, int64_t* n_weights);
-kb2e_status kb2e_renormalize(kb2e_ctx* ctx);
+/* Re-apply the per-row norm constraints of the model after a merge, to the
+ * rows flagged non-zero in the host masks (NULL = every row): TransE rows and
+ * TransH entity/relation rows are shrunk to length <= 1 (common/utils.cpp:70-77),
+ * TransH normals and TransR entity/relation/matrix rows scaled to unit length
+ * (transh/trainer.cpp:52, transr/trainer.cpp:174-180).  Weight masks are per
+ * relation. */
+kb2e_status kb2e_renormalize(kb2e_ctx* ctx, const uint8_t* entity_rows, const uint8_t* relation_rows,
+                             const uint8_t* weight_rows);
 
 #ifdef __cplusplus
 }

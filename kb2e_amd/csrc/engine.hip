@@ -30,6 +30,7 @@
 #include "kernels_index.hpp"
 #include "kernels_transe.hpp"
 #include "kernels_relowner.hpp"
+#include "kernels_sampler.hpp"
 
 using namespace kb2e;
 
@@ -102,13 +103,26 @@ struct kb2e_ctx {
     int64_t w_elems = 0;  // logical elements (TransH R*n, TransR R*n*n)
     // triples
     DevBuf heads, tails, rels;
-    // epoch sample stream
-    DevBuf si, sj, side;
-    std::vector<int32_t> h_si, h_sj;
-    std::vector<uint8_t> h_side;
+    // epoch sample stream, double-buffered: set `cur` feeds the epoch being
+    // trained, set cur^1 receives the next epoch's stream (device sampler).
+    DevBuf si_[2], sj_[2], side_[2];
+    int cur = 0;
     int32_t* pin_si = nullptr;
     int32_t* pin_sj = nullptr;
     uint8_t* pin_side = nullptr;
+    // device sampler (KB2E_SAMPLER_GLIBC): raw words of the glibc stream are
+    // made on the host, the rejection chain is resolved on the device.
+    hipStream_t side_stream = nullptr;
+    DevBuf words, levels, jfin, sidefin, filter_slots, pr_dev, consumed_dev;
+    int32_t* pin_words = nullptr;
+    int64_t* pin_consumed = nullptr;
+    std::vector<uint32_t> raw_vals;
+    int64_t nraw = 0, nraw_cap = 0;
+    double words_per_sample = 6.0;
+    bool prefetch_valid = false;   // set cur^1 holds the stream for the current rng state
+    uint64_t rng_version = 0, prefetch_version = 0;
+    hipEvent_t ev_sampled = nullptr, ev_epoch_done = nullptr;
+    bool host_sampler = false;     // KB2E_HOST_SAMPLER=1: draw on the host (debug)
     // replay stream supplied by the caller
     std::vector<int32_t> rp_si, rp_sj;
     std::vector<uint8_t> rp_side;
@@ -147,12 +161,20 @@ struct kb2e_ctx {
         if (pin_si) (void)hipHostFree(pin_si);
         if (pin_sj) (void)hipHostFree(pin_sj);
         if (pin_side) (void)hipHostFree(pin_side);
+        if (pin_words) (void)hipHostFree(pin_words);
+        if (pin_consumed) (void)hipHostFree(pin_consumed);
         flush_timers();
+        if (ev_sampled) (void)hipEventDestroy(ev_sampled);
+        if (ev_epoch_done) (void)hipEventDestroy(ev_epoch_done);
+        if (side_stream) (void)hipStreamDestroy(side_stream);
         for (auto e : event_pool) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
     bool f64() const { return cfg.precision == 64; }
+    int32_t* si() const { return si_[cur].as<int32_t>(); }
+    int32_t* sj() const { return sj_[cur].as<int32_t>(); }
+    uint8_t* side() const { return side_[cur].as<uint8_t>(); }
 
     hipEvent_t get_event() {
         if (!event_pool.empty()) {
@@ -266,9 +288,9 @@ void build_index(kb2e_ctx* c) {
     ka.heads = c->heads.as<int32_t>();
     ka.tails = c->tails.as<int32_t>();
     ka.rels = c->rels.as<int32_t>();
-    ka.si = c->si.as<int32_t>();
-    ka.sj = c->sj.as<int32_t>();
-    ka.side = c->side.as<uint8_t>();
+    ka.si = c->si();
+    ka.sj = c->sj();
+    ka.side = c->side();
     ka.owner = c->cfg.model == KB2E_TRANSE ? nullptr : c->owner.as<int32_t>();
     ka.nsamples = c->S;
     ka.B = (int32_t)c->B;
@@ -306,23 +328,145 @@ void build_index(kb2e_ctx* c) {
 
 // ----------------------------------------------------------------- sampling
 
-void sample_epoch(kb2e_ctx* c) {
-    if (c->cfg.sampler == KB2E_SAMPLER_REPLAY) {
-        if (c->rp_pos + c->S > (int64_t)c->rp_si.size())
-            throw std::invalid_argument("replay stream exhausted: supply a full epoch of samples");
-        std::memcpy(c->pin_si, c->rp_si.data() + c->rp_pos, c->S * sizeof(int32_t));
-        std::memcpy(c->pin_sj, c->rp_sj.data() + c->rp_pos, c->S * sizeof(int32_t));
-        std::memcpy(c->pin_side, c->rp_side.data() + c->rp_pos, c->S);
-        c->rp_pos += c->S;
-    } else {
-        for (int64_t k = 0; k < c->S; ++k) {
-            if (!HostSampler::draw(c->rng, c->ts, c->cfg.method, c->pin_si[k], c->pin_sj[k], c->pin_side[k]))
-                throw std::runtime_error("negative sampler cannot terminate: every entity completes a training triple");
-        }
+void upload_stream(kb2e_ctx* c, int set, hipStream_t st) {
+    HIPCHK(hipMemcpyAsync(c->si_[set].p, c->pin_si, c->S * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->sj_[set].p, c->pin_sj, c->S * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->side_[set].p, c->pin_side, c->S, hipMemcpyHostToDevice, st));
+}
+
+void ensure_sampler_capacity(kb2e_ctx* c, int64_t nraw) {
+    if (nraw <= c->nraw_cap) return;
+    const int K = std::max(1, bits_for(std::max<int64_t>(c->S - 1, 1)));
+    c->words.alloc(nraw * 4);
+    c->levels.alloc((size_t)K * (nraw + 1) * 4);
+    c->jfin.alloc(nraw * 4);
+    c->sidefin.alloc(nraw);
+    if (c->pin_words) (void)hipHostFree(c->pin_words);
+    HIPCHK(hipHostMalloc((void**)&c->pin_words, nraw * 4, 0));
+    c->raw_vals.resize(nraw);
+    c->nraw_cap = nraw;
+}
+
+// Draw the stream of the epoch that follows the committed rng state into set
+// cur^1, on the side stream: host makes the raw glibc words, the device
+// resolves the rejection chain (kernels_sampler.hpp).  Nothing is committed
+// until start_epoch consumes it.
+void launch_prefetch(kb2e_ctx* c) {
+    const int set = c->cur ^ 1;
+    const int64_t nraw = (int64_t)(c->words_per_sample * c->S) + 4096;
+    ensure_sampler_capacity(c, nraw);
+    c->nraw = nraw;
+    GlibcRand g = c->rng;
+    for (int64_t q = 0; q < nraw; ++q) {
+        const uint32_t v = g.next_raw();
+        c->raw_vals[q] = v;
+        c->pin_words[q] = (int32_t)(v >> 1);
     }
-    HIPCHK(hipMemcpyAsync(c->si.p, c->pin_si, c->S * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->sj.p, c->pin_sj, c->S * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->side.p, c->pin_side, c->S, hipMemcpyHostToDevice, c->stream));
+    hipStream_t st = c->side_stream;
+    // set cur^1 may still be read by the epoch before the current one
+    HIPCHK(hipStreamWaitEvent(st, c->ev_epoch_done, 0));
+    HIPCHK(hipMemcpyAsync(c->words.p, c->pin_words, nraw * 4, hipMemcpyHostToDevice, st));
+    const int K = std::max(1, bits_for(std::max<int64_t>(c->S - 1, 1)));
+    SamplerArgs a{};
+    a.words = c->words.as<int32_t>();
+    a.nraw = nraw;
+    a.heads = c->heads.as<int32_t>();
+    a.tails = c->tails.as<int32_t>();
+    a.rels = c->rels.as<int32_t>();
+    a.ntrain = (int32_t)c->ts.size();
+    a.ne = c->cfg.num_entities;
+    a.pr = c->pr_dev.as<double>();
+    a.slots = c->filter_slots.as<uint64_t>();
+    a.mask = c->ts.filter.mask;
+    a.nr64 = (uint64_t)c->cfg.num_relations;
+    a.ne64 = (uint64_t)c->cfg.num_entities;
+    a.next = c->levels.as<int32_t>();
+    a.jfin = c->jfin.as<int32_t>();
+    a.sidefin = c->sidefin.as<uint8_t>();
+    const int64_t stride = nraw + 1;
+    auto launch = [&] {
+        sample_len_kernel<<<(int)((stride + 255) / 256), 256, 0, st>>>(a);
+        HIPCHK(hipGetLastError());
+        for (int k = 1; k < K; ++k) {
+            sample_double_kernel<<<(int)((stride + 255) / 256), 256, 0, st>>>(
+                c->levels.as<int32_t>() + (int64_t)(k - 1) * stride, c->levels.as<int32_t>() + (int64_t)k * stride,
+                stride);
+            HIPCHK(hipGetLastError());
+        }
+        ChainArgs ca{};
+        ca.levels = c->levels.as<int32_t>();
+        ca.K = K;
+        ca.stride = stride;
+        ca.nsamples = c->S;
+        ca.nraw = nraw;
+        ca.words = a.words;
+        ca.jfin = a.jfin;
+        ca.sidefin = a.sidefin;
+        ca.next = a.next;
+        ca.ntrain = a.ntrain;
+        ca.si = c->si_[set].as<int32_t>();
+        ca.sj = c->sj_[set].as<int32_t>();
+        ca.side = c->side_[set].as<uint8_t>();
+        ca.consumed = c->consumed_dev.as<int64_t>();
+        sample_chain_kernel<<<(int)((c->S + 255) / 256), 256, 0, st>>>(ca);
+        HIPCHK(hipGetLastError());
+    };
+    if (c->prof) {
+        hipEvent_t e0 = c->get_event(), e1 = c->get_event();
+        HIPCHK(hipEventRecord(e0, st));
+        launch();
+        HIPCHK(hipEventRecord(e1, st));
+        c->pending.push_back({"sample", e0, e1});
+    } else {
+        launch();
+    }
+    HIPCHK(hipMemcpyAsync(c->pin_consumed, c->consumed_dev.p, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(c->ev_sampled, st));
+    c->prefetch_valid = true;
+    c->prefetch_version = c->rng_version;
+}
+
+// Make set `cur` hold this epoch's stream and commit the rng past it.
+void start_epoch_stream(kb2e_ctx* c) {
+    if (c->cfg.sampler == KB2E_SAMPLER_REPLAY || c->host_sampler) {
+        if (c->cfg.sampler == KB2E_SAMPLER_REPLAY) {
+            if (c->rp_pos + c->S > (int64_t)c->rp_si.size())
+                throw std::invalid_argument("replay stream exhausted: supply a full epoch of samples");
+            std::memcpy(c->pin_si, c->rp_si.data() + c->rp_pos, c->S * sizeof(int32_t));
+            std::memcpy(c->pin_sj, c->rp_sj.data() + c->rp_pos, c->S * sizeof(int32_t));
+            std::memcpy(c->pin_side, c->rp_side.data() + c->rp_pos, c->S);
+            c->rp_pos += c->S;
+        } else {
+            for (int64_t k = 0; k < c->S; ++k)
+                if (!HostSampler::draw(c->rng, c->ts, c->cfg.method, c->pin_si[k], c->pin_sj[k], c->pin_side[k]))
+                    throw std::runtime_error("negative sampler cannot terminate: every entity completes a training triple");
+            c->rng_version++;
+        }
+        // the previous epoch may still read set cur: use the other set
+        c->cur ^= 1;
+        upload_stream(c, c->cur, c->stream);
+        HIPCHK(hipStreamSynchronize(c->stream));  // pinned buffers are reused next epoch
+        return;
+    }
+    for (int attempt = 0;; ++attempt) {
+        if (!c->prefetch_valid || c->prefetch_version != c->rng_version) launch_prefetch(c);
+        HIPCHK(hipEventSynchronize(c->ev_sampled));
+        const int64_t used = *c->pin_consumed;
+        if (used >= 0) {
+            c->rng.commit(c->raw_vals.data(), used);
+            c->rng_version++;
+            c->words_per_sample = std::max(c->words_per_sample, 1.02 * (double)used / (double)c->S);
+            break;
+        }
+        // the speculative word buffer ran out (long rejection runs): retry larger
+        c->prefetch_valid = false;
+        c->words_per_sample *= 1.5;
+        if (attempt > 20)
+            throw std::runtime_error("negative sampler cannot terminate: every entity completes a training triple");
+    }
+    c->prefetch_valid = false;
+    c->cur ^= 1;
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_sampled, 0));
 }
 
 // --------------------------------------------------------------- the batch
@@ -333,9 +477,9 @@ ScoreArgs<T> score_args(kb2e_ctx* c, int64_t b) {
     a.heads = c->heads.as<int32_t>();
     a.tails = c->tails.as<int32_t>();
     a.rels = c->rels.as<int32_t>();
-    a.si = c->si.as<int32_t>() + b * c->B;
-    a.sj = c->sj.as<int32_t>() + b * c->B;
-    a.side = c->side.as<uint8_t>() + b * c->B;
+    a.si = c->si() + b * c->B;
+    a.sj = c->sj() + b * c->B;
+    a.side = c->side() + b * c->B;
     a.B = (int32_t)c->B;
     a.n = c->n;
     a.ld = c->ld;
@@ -443,7 +587,7 @@ void run_batches(kb2e_ctx* c, int64_t count) {
     if (!c->have_triples || !c->have_params) throw std::logic_error("upload triples and params first");
     for (int64_t q = 0; q < count; ++q) {
         if (c->epoch_pos == 0 && !c->epoch_ready) {
-            sample_epoch(c);
+            start_epoch_stream(c);
             build_index(c);
             c->epoch_ready = true;
             c->reduced_upto = 0;
@@ -451,6 +595,11 @@ void run_batches(kb2e_ctx* c, int64_t count) {
         if (c->f64()) run_batch<double>(c, c->epoch_pos);
         else run_batch<float>(c, c->epoch_pos);
         if (++c->epoch_pos == c->nb) {
+            // Overlap the next epoch's sampling with this epoch's batches.  It
+            // writes the set the previous epoch read, so it waits for the
+            // previous epoch's end marker (recorded below for the next one).
+            if (c->cfg.sampler == KB2E_SAMPLER_GLIBC && !c->host_sampler) launch_prefetch(c);
+            HIPCHK(hipEventRecord(c->ev_epoch_done, c->stream));
             reduce_stats(c, c->S);
             c->epoch_pos = 0;
             c->epoch_ready = false;
@@ -484,9 +633,15 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     c->nb = g.num_batches;
     c->S = c->B * c->nb;
     if (c->B < 1) throw std::invalid_argument("fewer training triples than batches");
-    c->si.alloc(c->S * 4);
-    c->sj.alloc(c->S * 4);
-    c->side.alloc(c->S);
+    for (int q = 0; q < 2; ++q) {
+        c->si_[q].alloc(c->S * 4);
+        c->sj_[q].alloc(c->S * 4);
+        c->side_[q].alloc(c->S);
+    }
+    c->prefetch_valid = false;
+    c->nraw_cap = 0;
+    c->consumed_dev.alloc(16);
+    if (!c->pin_consumed) HIPCHK(hipHostMalloc((void**)&c->pin_consumed, 16, 0));
     if (c->pin_si) { (void)hipHostFree(c->pin_si); (void)hipHostFree(c->pin_sj); (void)hipHostFree(c->pin_side); }
     HIPCHK(hipHostMalloc((void**)&c->pin_si, c->S * 4, 0));
     HIPCHK(hipHostMalloc((void**)&c->pin_sj, c->S * 4, 0));
@@ -523,7 +678,8 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     c->stats.alloc(64);
     setup_relowner_buffers(c);
     c->device_bytes = 0;
-    for (DevBuf* d : {&c->ent, &c->rel, &c->w, &c->heads, &c->tails, &c->rels, &c->si, &c->sj, &c->side,
+    for (DevBuf* d : {&c->ent, &c->rel, &c->w, &c->heads, &c->tails, &c->rels, &c->si_[0], &c->sj_[0], &c->side_[0],
+                      &c->si_[1], &c->sj_[1], &c->side_[1], &c->filter_slots, &c->pr_dev,
                       &c->keys, &c->keys_sorted, &c->sort_tmp, &c->flags, &c->idx, &c->seg_start, &c->act,
                       &c->loss, &c->xbits, &c->xreal, &c->aux, &c->tickets, &c->ent_done, &c->wsnap})
         c->device_bytes += (int64_t)d->bytes;
@@ -532,6 +688,22 @@ void setup_epoch_buffers(kb2e_ctx* c) {
 }  // namespace
 
 #include "engine_relowner.inc"
+
+namespace {
+template <typename T, int CH>
+__global__ __launch_bounds__(256) void renorm_kernel(T* table, int64_t rows, int ld, int n, const uint8_t* mask,
+                                                     int div, bool ignore_short) {
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t r = wave; r < rows; r += nwaves) {
+        if (mask && !mask[r / div]) continue;
+        RowReg<T, CH> v;
+        v.load(table + r * ld, n);
+        v.norm(n, ignore_short);
+        v.store(table + r * ld, n);
+    }
+}
+}  // namespace
 
 // ================================================================== C ABI
 
@@ -572,6 +744,12 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
         if (g.device < 0 || g.device >= ndev) return fail(c.get(), KB2E_EDEVICE, "no such HIP device");
         HIPCHK(hipSetDevice(g.device));
         HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_sampled, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_epoch_done, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(c->ev_epoch_done, c->stream));
+        const char* hs = getenv("KB2E_HOST_SAMPLER");
+        c->host_sampler = hs && hs[0] == '1';
         setup_buffers(c.get());
         return KB2E_OK;
     });
@@ -599,6 +777,13 @@ kb2e_status kb2e_upload_triples(kb2e_ctx* c, const int32_t* h, const int32_t* t,
         HIPCHK(hipMemcpy(c->heads.p, h, count * 4, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(c->tails.p, t, count * 4, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(c->rels.p, r, count * 4, hipMemcpyHostToDevice));
+        c->filter_slots.alloc(c->ts.filter.slots.size() * 8);
+        HIPCHK(hipMemcpy(c->filter_slots.p, c->ts.filter.slots.data(), c->ts.filter.slots.size() * 8,
+                         hipMemcpyHostToDevice));
+        std::vector<double> pr(c->ts.pr);
+        if (c->cfg.method == 0) std::fill(pr.begin(), pr.end(), 500.0);  // common/trainer.cpp:84-86
+        c->pr_dev.alloc(pr.size() * 8);
+        HIPCHK(hipMemcpy(c->pr_dev.p, pr.data(), pr.size() * 8, hipMemcpyHostToDevice));
         if (c->cfg.model != KB2E_TRANSE) plan_owners(c->plan, c->ts, c->cfg.num_relations);
         setup_epoch_buffers(c);
         c->have_triples = true;
@@ -646,6 +831,7 @@ kb2e_status kb2e_init_params(kb2e_ctx* c, double* ent_out, double* rel_out, doub
                 for (int j = 0; j < n; ++j)
                     for (int k = 0; k < n; ++k) W[((size_t)i * n + j) * n + k] = (j == k) ? 1.0 : 0.0;
         }
+        c->rng_version++;
         upload_tables(c, E.data(), R.data(), c->w_elems ? W.data() : nullptr);
         if (ent_out) std::memcpy(ent_out, E.data(), E.size() * 8);
         if (rel_out) std::memcpy(rel_out, R.data(), R.size() * 8);
@@ -767,7 +953,11 @@ kb2e_status kb2e_train_epoch(kb2e_ctx* c, double* loss, int64_t* active) {
     });
 }
 
-int32_t kb2e_rng_next(kb2e_ctx* c) { return c ? c->rng.next() : -1; }
+int32_t kb2e_rng_next(kb2e_ctx* c) {
+    if (!c) return -1;
+    c->rng_version++;
+    return c->rng.next();
+}
 
 kb2e_status kb2e_profile_enable(kb2e_ctx* c, int32_t on) {
     return guarded(c, [&] {
@@ -802,8 +992,55 @@ kb2e_status kb2e_device_tables(kb2e_ctx* c, void** e, void** r, void** w, int64_
     });
 }
 
-kb2e_status kb2e_renormalize(kb2e_ctx* c) {
-    return guarded(c, [&] { return fail(c, KB2E_EUNSUPPORTED, "renormalize: not yet implemented"); });
+kb2e_status kb2e_renormalize(kb2e_ctx* c, const uint8_t* ent_rows, const uint8_t* rel_rows, const uint8_t* w_rows) {
+    return guarded(c, [&] {
+        HIPCHK(hipSetDevice(c->cfg.device));
+        const int model = c->cfg.model;
+        // (table, rows, host mask, mask divisor, ignore_short)
+        struct Job {
+            DevBuf* t;
+            int64_t rows;
+            const uint8_t* mask;
+            int64_t mask_rows;
+            int div;
+            bool ignore_short;
+        };
+        std::vector<Job> jobs;
+        const bool unit = model == KB2E_TRANSR;
+        jobs.push_back({&c->ent, c->cfg.num_entities, ent_rows, c->cfg.num_entities, 1, !unit});
+        jobs.push_back({&c->rel, c->cfg.num_relations, rel_rows, c->cfg.num_relations, 1, !unit});
+        if (model == KB2E_TRANSH) jobs.push_back({&c->w, c->cfg.num_relations, w_rows, c->cfg.num_relations, 1, false});
+        if (model == KB2E_TRANSR)
+            jobs.push_back({&c->w, (int64_t)c->cfg.num_relations * c->n, w_rows, c->cfg.num_relations, c->n, false});
+        DevBuf mbuf;
+        for (const Job& j : jobs) {
+            const uint8_t* dmask = nullptr;
+            if (j.mask) {
+                mbuf.alloc(j.mask_rows);
+                HIPCHK(hipMemcpyAsync(mbuf.p, j.mask, j.mask_rows, hipMemcpyHostToDevice, c->stream));
+                dmask = mbuf.as<uint8_t>();
+            }
+            const int grid = (int)std::min<int64_t>((j.rows + 3) / 4, 65535);
+            auto go = [&](auto tag, auto chtag) {
+                using T = decltype(tag);
+                constexpr int CH = decltype(chtag)::value;
+                renorm_kernel<T, CH><<<grid, 256, 0, c->stream>>>(j.t->as<T>(), j.rows, c->ld, c->n, dmask, j.div,
+                                                                  j.ignore_short);
+            };
+            if (c->f64()) {
+                if (c->ch == 1) go(double(), std::integral_constant<int, 1>());
+                else if (c->ch == 2) go(double(), std::integral_constant<int, 2>());
+                else go(double(), std::integral_constant<int, 4>());
+            } else {
+                if (c->ch == 1) go(float(), std::integral_constant<int, 1>());
+                else if (c->ch == 2) go(float(), std::integral_constant<int, 2>());
+                else go(float(), std::integral_constant<int, 4>());
+            }
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipStreamSynchronize(c->stream));
+        }
+        return KB2E_OK;
+    });
 }
 
 }  // extern "C"

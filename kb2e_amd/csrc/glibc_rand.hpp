@@ -55,12 +55,31 @@ struct GlibcRand {
         return result;
     }
 
-    // The 31 most recent raw words in generation order (oldest first).  The
-    // next raw word is window[0] + window[28] (r[i] = r[i-31] + r[i-3]).
-    void window(uint32_t out[kDeg]) const {
-        // state[f] is the oldest of the window (r[i-31] for the next output),
-        // followed cyclically by newer words.
-        for (int k = 0; k < kDeg; ++k) out[k] = (uint32_t)state[(f + k) % kDeg];
+    // One raw 32-bit word (the value random_r stores; rand() returns it >> 1).
+    inline uint32_t next_raw() {
+        uint32_t val = (uint32_t)state[f] + (uint32_t)state[r];
+        state[f] = (int32_t)val;
+        if (++f >= kDeg) {
+            f = 0;
+            ++r;
+        } else if (++r >= kDeg) {
+            r = 0;
+        }
+        return val;
+    }
+
+    // Advance this generator past `m` words whose raw values `vals[0..m)` were
+    // generated from exactly this state (f and r always move together, r = f - 3
+    // mod 31, and the word made at step q lands in slot (f + q) mod 31).
+    void commit(const uint32_t* vals, int64_t m) {
+        if (m < kDeg) {
+            for (int64_t q = 0; q < m; ++q) (void)next_raw();
+            return;
+        }
+        const int f0 = f;
+        for (int64_t q = m - kDeg; q < m; ++q) state[(f0 + q) % kDeg] = (int32_t)vals[q];
+        f = (int)((f0 + m) % kDeg);
+        r = (f + kDeg - kSep) % kDeg;
     }
 };
 

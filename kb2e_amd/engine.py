@@ -70,7 +70,7 @@ def lib():
             "kb2e_device_bytes": (i64, [vp]),
             "kb2e_device_tables": (i32, [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(i64),
                                          C.POINTER(i64), C.POINTER(i64)]),
-            "kb2e_renormalize": (i32, [vp]),
+            "kb2e_renormalize": (i32, [vp, u8p, u8p, u8p]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -202,6 +202,11 @@ class Engine:
         n = C.c_int64(0)
         self._check(lib().kb2e_profile_query(self.h, name.encode(), C.byref(ms), C.byref(n)), "profile_query")
         return ms.value, n.value
+
+    def renormalize(self, ent_rows=None, rel_rows=None, w_rows=None):
+        keep = [None if m is None else np.ascontiguousarray(m, dtype=np.uint8) for m in (ent_rows, rel_rows, w_rows)]
+        ptrs = [None if m is None else m.ctypes.data_as(C.POINTER(C.c_uint8)) for m in keep]
+        self._check(lib().kb2e_renormalize(self.h, *ptrs), "renormalize")
 
     def device_bytes(self):
         return lib().kb2e_device_bytes(self.h)

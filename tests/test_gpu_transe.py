@@ -137,3 +137,35 @@ def test_errors_are_loud():
     bad[0, 0] = ds.num_entities + 5
     with pytest.raises(Exception):
         eng.upload_triples(bad)
+
+
+def _dense_dataset(ne=50, nr=2, count=3000, seed=3):
+    rng = np.random.default_rng(seed)
+    keys = rng.choice(ne * ne * nr, size=count, replace=False)
+    h, rest = keys // (ne * nr), keys % (ne * nr)
+    t, r = rest // nr, rest % nr
+    tr = np.stack([h, t, r], 1).astype(np.int32)
+    return data.Dataset(ne, nr, tr, tr[:0], tr[:0])
+
+
+@pytest.mark.parametrize("method", [0, 1])
+def test_device_sampler_rejection_heavy(method):
+    """60% of the entity space completes a known triple: long rejection chains,
+    the speculative word buffer grows; the stream must still be the reference's."""
+    ds = _dense_dataset()
+    _oracle_vs_engine(ds, 16, 3, method=method, batches=7)
+
+
+def test_device_sampler_matches_host_sampler(monkeypatch):
+    ds = data.synthetic("small", seed=2)
+    outs = []
+    for host in ("0", "1"):
+        monkeypatch.setenv("KB2E_HOST_SAMPLER", host)
+        eng = Engine("E", 32, ds.num_entities, ds.num_relations, rate=0.01, batches=50, seed=12)
+        eng.upload_triples(ds.train)
+        eng.init_params()
+        stats = [eng.train_epoch() for _ in range(2)]
+        outs.append((stats, eng.download_params()[:2], [eng.rng_next() for _ in range(5)]))
+    (s0, t0, r0), (s1, t1, r1) = outs
+    assert s0 == s1 and r0 == r1
+    assert np.array_equal(t0[0], t1[0]) and np.array_equal(t0[1], t1[1])

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Summarise a tools/gpu_profile.sh run into profiles/ (committed evidence).
+
+Writes profiles/<tag>_<config>.md (kernel stats table + PMC traffic) and
+profiles/pmc_<config>_f<prec>.json (per-launch HBM bytes per kernel family,
+read by bench.py for roofline.traffic).
+
+HBM bytes per MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE are in KiB;
+on gfx950 FETCH_SIZE counts exactly half of a wide coalesced read, so the
+corrected read bytes are 2 * FETCH_SIZE * 1024 (uncalibrated for other access
+widths -- both raw and corrected values are recorded).
+"""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+FAMILY = {"transe_fold_kernel": "fold", "transe_score_kernel": "score", "relowner": "relowner",
+          "transh_score": "score", "transr_score": "score", "ticket": "tickets"}
+
+
+def family(name):
+    for k, v in FAMILY.items():
+        if k in name:
+            return v
+    return name
+
+
+def main(src, tag, config, prec):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    bench = open(os.path.join(src, "bench.json")).read().strip()
+    pmc = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        path = os.path.join(src, f"pmc_{c}", "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        agg = defaultdict(lambda: [0.0, 0])
+        for r in csv.DictReader(open(path)):
+            a = agg[family(r["Kernel_Name"])]
+            a[0] += float(r["Counter_Value"])
+            a[1] += 1
+        pmc[c] = {k: v[0] / max(1, v[1]) for k, v in agg.items()}  # KiB per launch
+    per_kernel = {}
+    for fam in set(pmc.get("FETCH_SIZE", {})) | set(pmc.get("WRITE_SIZE", {})):
+        f = pmc.get("FETCH_SIZE", {}).get(fam, 0.0) * 1024
+        w = pmc.get("WRITE_SIZE", {}).get(fam, 0.0) * 1024
+        per_kernel[fam] = {"fetch_bytes_raw": f, "write_bytes": w, "hbm_bytes_per_launch": 2 * f + w}
+    out_json = os.path.join(root, "profiles", f"pmc_{config}_f{prec}.json")
+    json.dump(per_kernel, open(out_json, "w"), indent=1, sort_keys=True)
+    lines = [f"# Profile {tag}: {config} (f{prec})", "", "Command: `tools/gpu_profile.sh` on one MI355X "
+             "(rocprofv3 --kernel-trace --stats; separate --pmc FETCH_SIZE / WRITE_SIZE passes).", "",
+             "## bench.py line", "", "```", bench, "```", "", "## Kernel stats (rocprofv3 --stats)", "",
+             "| kernel | calls | total ms | avg us | % |", "|---|---|---|---|---|"]
+    for r in stats[:16]:
+        lines.append(f"| {r['Name'][:60]} | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.2f} | "
+                     f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} |")
+    lines += ["", "## HBM traffic per launch (PMC, gfx950-corrected: 2 x FETCH_SIZE + WRITE_SIZE)", "",
+              "| kernel family | FETCH_SIZE raw (bytes) | WRITE_SIZE (bytes) | corrected HBM bytes |", "|---|---|---|---|"]
+    for fam, v in sorted(per_kernel.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"])[:12]:
+        lines.append(f"| {fam} | {v['fetch_bytes_raw']:.0f} | {v['write_bytes']:.0f} | {v['hbm_bytes_per_launch']:.0f} |")
+    md = os.path.join(root, "profiles", f"{tag}_{config}_f{prec}.md")
+    open(md, "w").write("\n".join(lines) + "\n")
+    print(md, out_json)
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:5])
