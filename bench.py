@@ -162,7 +162,7 @@ def main():
     eng.upload_triples(train)
     ent, rel, w = eng.init_params()
     if model == "R":
-        eng.upload_params(ent / np.linalg.norm(ent, axis=1, keepdims=True), rel, w)
+        eng.transr_seed(ent, rel)  # seed = the init draws (no TransE run in the bench)
     B = len(train) // batches
     merger = None
     if world > 1:

@@ -89,6 +89,12 @@ kb2e_status kb2e_upload_triples(kb2e_ctx* ctx, const int32_t* heads, const int32
  * R x n x n ([r][j][i]). */
 kb2e_status kb2e_init_params(kb2e_ctx* ctx, double* entity, double* relation, double* weights);
 
+/* TransR's seed step (transr/trainer.cpp:88-113): entity rows from the
+ * seed TransE run are scaled to unit length (common::norm(v, false)),
+ * relation rows are taken verbatim; the relation matrices keep the identity
+ * that kb2e_init_params set.  Call after kb2e_init_params. */
+kb2e_status kb2e_transr_seed(kb2e_ctx* ctx, const double* entity, const double* relation);
+
 /* Upload tables (row-major FP64 as in the reference's vectors).  `weights` may
  * be NULL for TransE.  Used for TransR seeding (transr/trainer.cpp:88-113; the
  * caller applies the entity unit norm as the reference does) and for restarts. */

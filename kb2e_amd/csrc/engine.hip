@@ -85,6 +85,9 @@ namespace {
 void setup_relowner_buffers(kb2e_ctx* c);
 template <typename T>
 void run_batch_relowner(kb2e_ctx* c, int64_t b);
+void check_dataflow(kb2e_ctx* c);
+void build_owner_index(kb2e_ctx* c);
+void prepare_relowner_kernels();
 }  // namespace
 
 struct kb2e_ctx {
@@ -135,10 +138,12 @@ struct kb2e_ctx {
     // phase A outputs
     DevBuf act, loss;      // [S]
     DevBuf xbits, xreal;   // [B][2][nw], [B][2][ld]
-    DevBuf aux;            // model-specific per-update exports
+    DevBuf aux, aux2;      // model-specific per-update exports
     // relation-owner schedule (TransH / TransR)
     RelOwnerPlan plan;
-    DevBuf owner, tickets, ent_done, wsnap, transr_work;
+    DevBuf owner, tickets, ent_done, wsnap, transr_work, owner_seg, dataflow_err, wtouched;
+    int num_cus = 256;
+    uint32_t batch_stamp = 0;
     // stats
     DevBuf stats;  // double loss, double active (reduced)
     double acc_loss = 0;
@@ -267,6 +272,12 @@ int64_t w_rows(const kb2e_ctx* c) {
     return 0;
 }
 
+void sync_wsnap(kb2e_ctx* c) {
+    if (c->cfg.model != KB2E_TRANSR) return;
+    HIPCHK(hipMemcpyAsync(c->wsnap.p, c->w.p, c->w.bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+}
+
 void upload_tables(kb2e_ctx* c, const double* e, const double* r, const double* w) {
     const int64_t ne = c->cfg.num_entities, nr = c->cfg.num_relations;
     if (c->f64()) {
@@ -278,6 +289,7 @@ void upload_tables(kb2e_ctx* c, const double* e, const double* r, const double* 
         if (r) upload_rows<float>(c, c->rel, r, nr, c->n, c->ld);
         if (w && w_rows(c)) upload_rows<float>(c, c->w, w, w_rows(c), c->n, c->ld);
     }
+    if (w) sync_wsnap(c);
 }
 
 // ------------------------------------------------------------------- index
@@ -323,6 +335,7 @@ void build_index(kb2e_ctx* c) {
                                                         c->nseg.as<int32_t>(), (int)c->nb, c->kl,
                                                         c->batch_seg.as<int32_t>());
         HIPCHK(hipGetLastError());
+        if (c->cfg.model != KB2E_TRANSE) build_owner_index(c);
     });
 }
 
@@ -581,6 +594,7 @@ void reduce_stats(kb2e_ctx* c, int64_t upto) {
     c->acc_loss += h[0];
     c->acc_active += (int64_t)llround(h[1]);
     c->reduced_upto = upto;
+    check_dataflow(c);
 }
 
 void run_batches(kb2e_ctx* c, int64_t count) {
@@ -623,6 +637,10 @@ void setup_buffers(kb2e_ctx* c) {
     if (g.model == KB2E_TRANSR) c->w_elems = (int64_t)g.num_relations * g.dim * g.dim;
     c->w.alloc((size_t)std::max<int64_t>(1, w_rows(c)) * c->ld * es);
     HIPCHK(hipMemset(c->w.p, 0, c->w.bytes));
+    if (g.model == KB2E_TRANSR) {  // committed matrices (start-of-batch snapshot)
+        c->wsnap.alloc(c->w.bytes);
+        HIPCHK(hipMemset(c->wsnap.p, 0, c->wsnap.bytes));
+    }
     c->device_bytes = (int64_t)(c->ent.bytes + c->rel.bytes + c->w.bytes);
 }
 
@@ -681,7 +699,7 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     for (DevBuf* d : {&c->ent, &c->rel, &c->w, &c->heads, &c->tails, &c->rels, &c->si_[0], &c->sj_[0], &c->side_[0],
                       &c->si_[1], &c->sj_[1], &c->side_[1], &c->filter_slots, &c->pr_dev,
                       &c->keys, &c->keys_sorted, &c->sort_tmp, &c->flags, &c->idx, &c->seg_start, &c->act,
-                      &c->loss, &c->xbits, &c->xreal, &c->aux, &c->tickets, &c->ent_done, &c->wsnap})
+                      &c->loss, &c->xbits, &c->xreal, &c->aux, &c->aux2, &c->tickets, &c->ent_done, &c->wsnap})
         c->device_bytes += (int64_t)d->bytes;
 }
 
@@ -735,6 +753,8 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
         (g.distance != 0 && g.distance != 1) || (g.sampler != 0 && g.sampler != 1))
         return KB2E_EINVAL;
     if (g.model == KB2E_TRANSR && g.num_relations > g.num_entities) return KB2E_EINVAL;  // entityVec_next_[relation]
+    if (g.model == KB2E_TRANSR && ((size_t)g.dim * (g.dim + 1) + 3 * (size_t)g.dim) * (g.precision / 8) > 96 * 1024)
+        return KB2E_EUNSUPPORTED;  // the owner's relation matrix must fit in LDS
     std::unique_ptr<kb2e_ctx> c(new kb2e_ctx());
     c->cfg = g;
     c->rng.seed_with(g.seed);
@@ -748,6 +768,8 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
         HIPCHK(hipEventCreateWithFlags(&c->ev_sampled, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->ev_epoch_done, hipEventDisableTiming));
         HIPCHK(hipEventRecord(c->ev_epoch_done, c->stream));
+        HIPCHK(hipDeviceGetAttribute(&c->num_cus, hipDeviceAttributeMultiprocessorCount, g.device));
+        prepare_relowner_kernels();
         const char* hs = getenv("KB2E_HOST_SAMPLER");
         c->host_sampler = hs && hs[0] == '1';
         setup_buffers(c.get());
@@ -784,7 +806,7 @@ kb2e_status kb2e_upload_triples(kb2e_ctx* c, const int32_t* h, const int32_t* t,
         if (c->cfg.method == 0) std::fill(pr.begin(), pr.end(), 500.0);  // common/trainer.cpp:84-86
         c->pr_dev.alloc(pr.size() * 8);
         HIPCHK(hipMemcpy(c->pr_dev.p, pr.data(), pr.size() * 8, hipMemcpyHostToDevice));
-        if (c->cfg.model != KB2E_TRANSE) plan_owners(c->plan, c->ts, c->cfg.num_relations);
+        if (c->cfg.model != KB2E_TRANSE) plan_owners(c->plan, c->ts, c->cfg.num_relations, c->num_cus);
         setup_epoch_buffers(c);
         c->have_triples = true;
         c->epoch_pos = 0;
@@ -837,6 +859,25 @@ kb2e_status kb2e_init_params(kb2e_ctx* c, double* ent_out, double* rel_out, doub
         if (rel_out) std::memcpy(rel_out, R.data(), R.size() * 8);
         if (w_out && c->w_elems) std::memcpy(w_out, W.data(), (size_t)c->w_elems * 8);
         c->have_params = true;
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_transr_seed(kb2e_ctx* c, const double* e, const double* r) {
+    return guarded(c, [&] {
+        if (c->cfg.model != KB2E_TRANSR) return fail(c, KB2E_EUNSUPPORTED, "TransR only");
+        if (!e || !r) return fail(c, KB2E_EINVAL, "entity and relation seed tables required");
+        HIPCHK(hipSetDevice(c->cfg.device));
+        const int n = c->n;
+        std::vector<double> E(e, e + (size_t)c->cfg.num_entities * n);
+        for (int64_t i = 0; i < c->cfg.num_entities; ++i) {  // common::norm(entityVec_[i], false)
+            double* a = &E[(size_t)i * n];
+            double res = 0;
+            for (int j = 0; j < n; ++j) res += a[j] * a[j];
+            const double len = std::sqrt(res);
+            for (int j = 0; j < n; ++j) a[j] /= len;
+        }
+        upload_tables(c, E.data(), r, nullptr);
         return KB2E_OK;
     });
 }
@@ -1039,6 +1080,7 @@ kb2e_status kb2e_renormalize(kb2e_ctx* c, const uint8_t* ent_rows, const uint8_t
             HIPCHK(hipGetLastError());
             HIPCHK(hipStreamSynchronize(c->stream));
         }
+        sync_wsnap(c);
         return KB2E_OK;
     });
 }

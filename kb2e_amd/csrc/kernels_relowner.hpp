@@ -1,4 +1,31 @@
-// kernels_relowner.hpp -- relation-owner schedule for TransH / TransR (plan).
+// kernels_relowner.hpp -- exact TransH / TransR batches: relation-owner
+// dataflow with per-entity tickets.
+//
+// In TransH and TransR the reference couples rows inside a batch: after every
+// gradientUpdate it re-orthogonalises entity rows against the relation's
+// normal (transh/trainer.cpp:56-58, common/utils.cpp:79-111) or re-projects
+// them through the relation matrix (transRNorm, transr/trainer.cpp:35-64,
+// 185-187), and those loops also modify the relation state.  The order of
+// updates therefore matters across rows.  We replay it exactly:
+//
+//   * every relation belongs to one persistent "owner" workgroup (LPT-balanced
+//     on relation frequency); an owner replays its relations' updates in
+//     global sample order, holding the relation state (r, w / Mr) itself;
+//   * every entity row touched in the batch carries a ticket counter; an
+//     update may touch entity e only when e's counter equals the number of
+//     earlier active updates on e (computed by ticket_kernel from the sorted
+//     event index), and bumps it afterwards.
+//
+// Because each owner walks its list in increasing global order and every
+// dependency points to an earlier update, the earliest unfinished update is
+// always runnable: no deadlock with all owners resident (grid <= #CUs, one
+// workgroup per CU).  Entity rows move between owners through write-through
+// (sc1) stores drained by s_waitcnt vmcnt(0) before an agent-scope atomic
+// flag, and sc1 loads after the poll (MI355X_MICROARCH.md "Valid forms").
+//
+// Phase A (score) exports everything the updates need from the start-of-batch
+// snapshot, so phase B never reads a snapshot row another owner may have
+// already advanced.
 #pragma once
 
 #include <algorithm>
@@ -10,21 +37,16 @@
 
 namespace kb2e {
 
-// Relations are dealt to persistent "owner" workgroups by LPT bin packing on
-// their training-triple counts, so the hottest relations get a workgroup of
-// their own.  Every owner replays its relations' updates in global sample
-// order, which is what makes the per-entity ticket protocol deadlock-free.
 struct RelOwnerPlan {
     int num_owners = 0;
     std::vector<int32_t> owner;  // relation -> owner
 };
 
-inline void plan_owners(RelOwnerPlan& p, const TripleStore& ts, int num_relations, int max_owners = 256) {
+inline void plan_owners(RelOwnerPlan& p, const TripleStore& ts, int num_relations, int max_owners) {
     p.num_owners = std::max(1, std::min(num_relations, max_owners));
     std::vector<int> order(num_relations);
     std::iota(order.begin(), order.end(), 0);
-    std::stable_sort(order.begin(), order.end(),
-                     [&](int a, int b) { return ts.rel_count[a] > ts.rel_count[b]; });
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return ts.rel_count[a] > ts.rel_count[b]; });
     std::vector<int64_t> load(p.num_owners, 0);
     p.owner.assign(num_relations, 0);
     for (int r : order) {
@@ -34,4 +56,789 @@ inline void plan_owners(RelOwnerPlan& p, const TripleStore& ts, int num_relation
     }
 }
 
+// ------------------------------------------------------------- coherence
+
+using gu64 = __attribute__((address_space(1))) uint64_t;
+using gu32 = __attribute__((address_space(1))) uint32_t;
+
+template <typename T>
+__device__ __forceinline__ T load_sc1(const T* p) {
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t b = __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return __builtin_bit_cast(T, b);
+    } else {
+        const uint32_t b = __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return __builtin_bit_cast(T, b);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void store_sc1(T* p, T v) {
+    if constexpr (sizeof(T) == 8)
+        __hip_atomic_store((gu64*)p, __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        __hip_atomic_store((gu32*)p, __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename T, int CH>
+__device__ __forceinline__ void row_load_sc1(RowReg<T, CH>& R, const T* row, int n) {
+    const int l = lane_id();
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int e = c * (kWave * kVec) + l * kVec;
+        R.v[c][0] = e < n ? load_sc1(row + e) : T(0);
+        R.v[c][1] = e + 1 < n ? load_sc1(row + e + 1) : T(0);
+    }
+}
+
+template <typename T, int CH>
+__device__ __forceinline__ void row_store_sc1(const RowReg<T, CH>& R, T* row, int n) {
+    const int l = lane_id();
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int e = c * (kWave * kVec) + l * kVec;
+        if (e < n) store_sc1(row + e, R.v[c][0]);
+        if (e + 1 < n) store_sc1(row + e + 1, R.v[c][1]);
+    }
+}
+
+// Wait until done[e] == ticket (bounded; a timeout sets *err and gives up).
+__device__ __forceinline__ void wait_ticket(const uint32_t* done, int e, uint32_t ticket, uint32_t* err) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load((gu32*)(done + e), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ticket) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 26)) {
+            __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+}
+
+__device__ __forceinline__ void release_ticket(uint32_t* done, int e, uint32_t ticket) {
+    if (lane_id() == 0)
+        __hip_atomic_store((gu32*)(done + e), ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// ------------------------------------------------------------- tickets
+
+struct TicketArgs {
+    const uint64_t* keys;
+    const int32_t* seg_start;
+    const int32_t* batch_seg;
+    int32_t batch;
+    KeyLayout kl;
+    int32_t ne;
+    const uint8_t* act;  // [B]
+    uint32_t* tickets;   // [B][2][3]
+    uint32_t* done;      // [ne]
+};
+
+// One wave per entity segment: ticket = number of earlier active updates on
+// the entity in this batch; resets the entity's counter.
+__global__ __launch_bounds__(256) void ticket_kernel(TicketArgs a) {
+    const int s0 = a.batch_seg[a.batch], s1 = a.batch_seg[a.batch + 1];
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int nwaves = (gridDim.x * blockDim.x) >> 6;
+    const int l = lane_id();
+    for (int s = s0 + wave; s < s1; s += nwaves) {
+        const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
+        const int row = a.kl.row_of(a.keys[p0]);
+        if (row >= a.ne) continue;  // owner segments
+        if (l == 0) a.done[row] = 0;
+        uint32_t count = 0;
+        for (int base = p0; base < p1; base += kWave) {
+            const int p = base + l;
+            uint64_t key = 0;
+            bool active = false;
+            if (p < p1) {
+                key = a.keys[p];
+                active = a.act[a.kl.kk_of(key)] != 0;
+            }
+            const uint64_t m = __ballot(active);
+            const uint32_t before = (uint32_t)__popcll(m & ((1ull << l) - 1ull));
+            if (active) {
+                const int kk = a.kl.kk_of(key), u = (int)((key >> 3) & 1);
+                const uint32_t roles = (uint32_t)(key & 7);
+                uint32_t* t = a.tickets + ((int64_t)kk * 2 + u) * 3;
+                if (roles & kRoleHead) t[0] = count + before;
+                if (roles & kRoleTail) t[1] = count + before;
+                if (roles & kRoleEntRel) t[2] = count + before;
+            }
+            count += (uint32_t)__popcll(m);
+        }
+    }
+}
+
+// owner_seg[b * owners + o] = segment of owner o in batch b (or -1).
+__global__ __launch_bounds__(256) void owner_seg_kernel(const uint64_t* keys, const int32_t* seg_start,
+                                                        const int32_t* nseg_p, KeyLayout kl, int32_t ne,
+                                                        int32_t owners, int32_t* owner_seg) {
+    const int nseg = *nseg_p;
+    for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x) {
+        const uint64_t k = keys[seg_start[s]];
+        const int row = kl.row_of(k);
+        if (row >= ne) owner_seg[(int64_t)kl.batch_of(k) * owners + (row - ne)] = s;
+    }
+}
+
+// ---------------------------------------------------------- TransH phase A
+
+template <typename T>
+struct HScoreArgs {
+    const int32_t* heads;
+    const int32_t* tails;
+    const int32_t* rels;
+    const int32_t* si;
+    const int32_t* sj;
+    const uint8_t* side;
+    int32_t B, n, ld, nw;
+    const T* ent;
+    const T* rel;
+    const T* w;
+    double margin;
+    uint8_t* act;
+    double* loss;
+    uint64_t* xbits;  // [B][2][nw]
+    T* scal;          // [B][2][4]: headSum, tailSum, sum_x
+    T* snap;          // [B][2][2][ld]: snapshot head row, tail row
+};
+
+// transh/transh.cpp:10-29 energies, transh/trainer.cpp:14-33 directions.
+template <typename T, int CH>
+__global__ __launch_bounds__(256) void transh_score_kernel(HScoreArgs<T> a) {
+    const int kk = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (kk >= a.B) return;
+    const int l = lane_id();
+    const int i = a.si[kk], j = a.sj[kk];
+    const int h = a.heads[i], t = a.tails[i], r = a.rels[i];
+    const int nh = a.side[kk] ? h : j, nt = a.side[kk] ? j : t;
+    RowReg<T, CH> H, Tt, R, W, NH, NT;
+    H.load(a.ent + (int64_t)h * a.ld, a.n);
+    Tt.load(a.ent + (int64_t)t * a.ld, a.n);
+    R.load(a.rel + (int64_t)r * a.ld, a.n);
+    W.load(a.w + (int64_t)r * a.ld, a.n);
+    NH.load(a.ent + (int64_t)nh * a.ld, a.n);
+    NT.load(a.ent + (int64_t)nt * a.ld, a.n);
+    T hs_p = T(0), ts_p = T(0), hs_n = T(0), ts_n = T(0);
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            hs_p += W.v[c][k] * H.v[c][k];
+            ts_p += W.v[c][k] * Tt.v[c][k];
+            hs_n += W.v[c][k] * NH.v[c][k];
+            ts_n += W.v[c][k] * NT.v[c][k];
+        }
+    hs_p = wave_sum(hs_p);
+    ts_p = wave_sum(ts_p);
+    hs_n = wave_sum(hs_n);
+    ts_n = wave_sum(ts_n);
+    T dp[CH][kVec], dn[CH][kVec];
+    T ep = T(0), en = T(0);
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            dp[c][k] = Tt.v[c][k] - ts_p * W.v[c][k] - (H.v[c][k] - hs_p * W.v[c][k]) - R.v[c][k];
+            dn[c][k] = NT.v[c][k] - ts_n * W.v[c][k] - (NH.v[c][k] - hs_n * W.v[c][k]) - R.v[c][k];
+            ep += fabs(dp[c][k]);
+            en += fabs(dn[c][k]);
+        }
+    ep = wave_sum(ep);
+    en = wave_sum(en);
+    const double e_pos = (double)ep, e_neg = (double)en;
+    const bool active = e_pos + a.margin > e_neg;
+    if (l == 0) {
+        a.act[kk] = active ? 1 : 0;
+        a.loss[kk] = active ? a.margin + e_pos - e_neg : 0.0;
+    }
+    if (!active) return;
+    // sum_x = sum_i x_i w_i with x_i = +-1 (transh/trainer.cpp:33)
+    T sx_p = T(0), sx_n = T(0);
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            if (!elem_valid(c, k, a.n)) continue;
+            sx_p += (dp[c][k] > T(0) ? T(1) : T(-1)) * W.v[c][k];
+            sx_n += (dn[c][k] > T(0) ? T(1) : T(-1)) * W.v[c][k];
+        }
+    sx_p = wave_sum(sx_p);
+    sx_n = wave_sum(sx_n);
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            const bool valid = elem_valid(c, k, a.n);
+            const uint64_t bp = __ballot(valid && dp[c][k] > T(0));
+            const uint64_t bn = __ballot(valid && dn[c][k] > T(0));
+            if (l == 0) {
+                a.xbits[((int64_t)kk * 2 + 0) * a.nw + c * kVec + k] = bp;
+                a.xbits[((int64_t)kk * 2 + 1) * a.nw + c * kVec + k] = bn;
+            }
+        }
+    if (l == 0) {
+        T* s0 = a.scal + ((int64_t)kk * 2 + 0) * 4;
+        T* s1 = a.scal + ((int64_t)kk * 2 + 1) * 4;
+        s0[0] = hs_p; s0[1] = ts_p; s0[2] = sx_p;
+        s1[0] = hs_n; s1[1] = ts_n; s1[2] = sx_n;
+    }
+    H.store(a.snap + (((int64_t)kk * 2 + 0) * 2 + 0) * a.ld, a.n);
+    Tt.store(a.snap + (((int64_t)kk * 2 + 0) * 2 + 1) * a.ld, a.n);
+    NH.store(a.snap + (((int64_t)kk * 2 + 1) * 2 + 0) * a.ld, a.n);
+    NT.store(a.snap + (((int64_t)kk * 2 + 1) * 2 + 1) * a.ld, a.n);
+}
+
+// common/utils.cpp:79-111 norm(a, b, rate) on registers, with the
+// reference's running `sum` (never reset between iterations).
+template <typename T, int CH>
+__device__ __forceinline__ void orth_norm(RowReg<T, CH>& A, RowReg<T, CH>& Bv, int n, T rate) {
+    Bv.norm(n, false);
+    T sum = T(0);
+    for (int it = 0; it < 1 << 20; ++it) {
+        sum += Bv.sumsq();
+        sum = sqrt(sum);
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k)
+                if (elem_valid(c, k, n)) Bv.v[c][k] = Bv.v[c][k] / sum;
+        T x = T(0);
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) x += Bv.v[c][k] * A.v[c][k];
+        x = wave_sum(x);
+        if (!(x > T(0.1))) break;
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) {
+                if (!elem_valid(c, k, n)) continue;
+                A.v[c][k] = A.v[c][k] - rate * Bv.v[c][k];
+                Bv.v[c][k] = Bv.v[c][k] - rate * A.v[c][k];
+            }
+    }
+    Bv.norm(n, false);
+}
+
+// ---------------------------------------------------------- TransH phase B
+
+template <typename T>
+struct OwnerArgs {
+    const uint64_t* keys;
+    const int32_t* seg_start;
+    const int32_t* owner_seg;  // [nb][owners]
+    int32_t batch, owners;
+    KeyLayout kl;
+    int32_t n, ld, nw;
+    const int32_t* heads;
+    const int32_t* tails;
+    const int32_t* rels;
+    const int32_t* si;
+    const int32_t* sj;
+    const uint8_t* side;
+    const uint8_t* act;
+    const uint32_t* tickets;
+    uint32_t* done;
+    uint32_t* err;
+    T* ent;
+    T* rel;
+    T* w;        // TransH normals (live) / TransR matrices: next (W_B)
+    const T* wsnap;  // TransR: matrices at batch start (W_A)
+    uint32_t* wtouched;  // TransR: relation -> batch stamp
+    double lr;
+    const uint64_t* xbits;
+    const T* xreal;
+    const T* scal;
+    const T* snap;
+};
+
+struct UpdateIds {
+    int kk, u, r;
+    int ent[3];       // distinct entities (head first), -1 unused
+    uint32_t roles[3];
+    uint32_t tick[3];
+    int count;
+};
+
+template <typename T>
+__device__ __forceinline__ UpdateIds decode_update(const OwnerArgs<T>& a, uint64_t key, bool entrel) {
+    UpdateIds d;
+    d.kk = a.kl.kk_of(key);
+    d.u = (int)((key >> 3) & 1);
+    const int i = a.si[d.kk], j = a.sj[d.kk];
+    const int h = a.heads[i], t = a.tails[i];
+    d.r = a.rels[i];
+    int eh = h, et = t;
+    if (d.u == 1) {
+        if (a.side[d.kk]) et = j;
+        else eh = j;
+    }
+    const int ids[3] = {eh, et, entrel ? d.r : -1};
+    const uint32_t rl[3] = {kRoleHead, kRoleTail, kRoleEntRel};
+    const uint32_t* tk = a.tickets + ((int64_t)d.kk * 2 + d.u) * 3;
+    d.count = 0;
+    for (int q = 0; q < 3; ++q) {
+        if (ids[q] < 0) continue;
+        int found = -1;
+        for (int p = 0; p < d.count; ++p)
+            if (d.ent[p] == ids[q]) found = p;
+        if (found >= 0) {
+            d.roles[found] |= rl[q];
+        } else {
+            d.ent[d.count] = ids[q];
+            d.roles[d.count] = rl[q];
+            d.tick[d.count] = tk[q];
+            ++d.count;
+        }
+    }
+    return d;
+}
+
+template <typename T, int CH>
+__global__ __launch_bounds__(64) void transh_owner_kernel(OwnerArgs<T> a) {
+    const int seg = a.owner_seg[(int64_t)a.batch * a.owners + blockIdx.x];
+    if (seg < 0) return;
+    const int p0 = a.seg_start[seg], p1 = a.seg_start[seg + 1];
+    const int n = a.n;
+    const T lr = (T)a.lr;
+    for (int p = p0; p < p1; ++p) {
+        const uint64_t key = a.keys[p];
+        const int kk = a.kl.kk_of(key);
+        if (!a.act[kk]) continue;
+        const UpdateIds d = decode_update(a, key, false);
+        for (int q = 0; q < d.count; ++q) wait_ticket(a.done, d.ent[q], d.tick[q], a.err);
+        RowReg<T, CH> E0, E1, R, W;
+        row_load_sc1(E0, a.ent + (int64_t)d.ent[0] * a.ld, n);
+        if (d.count > 1) row_load_sc1(E1, a.ent + (int64_t)d.ent[1] * a.ld, n);
+        R.load(a.rel + (int64_t)d.r * a.ld, n);
+        W.load(a.w + (int64_t)d.r * a.ld, n);
+        // head row = E0; tail row = E0 (h == t) or E1
+        const bool same = d.count == 1;
+        const T* sc = a.scal + ((int64_t)kk * 2 + d.u) * 4;
+        const T hs = sc[0], ts = sc[1], sumx = sc[2];
+        const uint64_t* xw = a.xbits + ((int64_t)kk * 2 + d.u) * a.nw;
+        uint64_t words[2 * CH];
+#pragma unroll
+        for (int q = 0; q < 2 * CH; ++q) words[q] = xw[q];
+        const T beta = d.u ? T(1) : T(-1);
+        const T blr = beta * lr;  // beta * learningRate_
+        RowReg<T, CH> SH, ST;     // snapshot head / tail rows
+        SH.load(a.snap + (((int64_t)kk * 2 + d.u) * 2 + 0) * a.ld, n);
+        ST.load(a.snap + (((int64_t)kk * 2 + d.u) * 2 + 1) * a.ld, n);
+        // transh/trainer.cpp:23-41
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) {
+                if (!elem_valid(c, k, n)) continue;
+                const T x = xbit(words, c, k) ? T(1) : T(-1);
+                const T dlt = blr * x;
+                R.v[c][k] = R.v[c][k] - dlt;
+                E0.v[c][k] = E0.v[c][k] - dlt;
+                if (same) E0.v[c][k] = E0.v[c][k] + dlt;
+                else E1.v[c][k] = E1.v[c][k] + dlt;
+                W.v[c][k] = W.v[c][k] + dlt * hs;
+                W.v[c][k] = W.v[c][k] - dlt * ts;
+            }
+        // transh/trainer.cpp:43-46
+        const T g = blr * sumx;
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) {
+                if (!elem_valid(c, k, n)) continue;
+                W.v[c][k] = W.v[c][k] + g * SH.v[c][k];
+                W.v[c][k] = W.v[c][k] - g * ST.v[c][k];
+            }
+        // transh/trainer.cpp:48-58
+        R.norm(n, true);
+        E0.norm(n, true);
+        if (same) E0.norm(n, true);
+        else E1.norm(n, true);
+        W.norm(n, false);
+        orth_norm(R, W, n, lr);
+        orth_norm(E0, W, n, lr);
+        if (same) orth_norm(E0, W, n, lr);
+        else orth_norm(E1, W, n, lr);
+        R.store(a.rel + (int64_t)d.r * a.ld, n);
+        W.store(a.w + (int64_t)d.r * a.ld, n);
+        row_store_sc1(E0, a.ent + (int64_t)d.ent[0] * a.ld, n);
+        if (!same) row_store_sc1(E1, a.ent + (int64_t)d.ent[1] * a.ld, n);
+        drain_stores();
+        for (int q = 0; q < d.count; ++q) release_ticket(a.done, d.ent[q], d.tick[q]);
+    }
+}
+
+
+// ---------------------------------------------------------- TransR phase A
+
+template <typename T>
+struct RScoreArgs {
+    const int32_t* heads;
+    const int32_t* tails;
+    const int32_t* rels;
+    const int32_t* si;
+    const int32_t* sj;
+    const uint8_t* side;
+    int32_t B, n, ld;
+    const T* ent;
+    const T* rel;
+    const T* W;       // matrices at batch start, rows [r * n + j] of length ld
+    double margin;
+    int32_t compat, l1;
+    uint8_t* act;
+    double* loss;
+    T* x;             // [B][2][ld] update directions (+-1 for L1)
+    T* d;             // [B][2][ld] snapshot head - tail
+    double* proj;     // [B][2][2][ld] W^T head, W^T tail per energy call (compat)
+};
+
+// transr/transr.cpp:13-37 (projections summed over j in the reference's order)
+// and transr/trainer.cpp:147-164 (x from fresh projections).
+template <typename T, int CH>
+__global__ __launch_bounds__(256) void transr_project_kernel(RScoreArgs<T> a) {
+    const int kk = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (kk >= a.B) return;
+    const int l = lane_id();
+    const int n = a.n;
+    const int i0 = a.si[kk], jj = a.sj[kk];
+    const int h = a.heads[i0], t = a.tails[i0], r = a.rels[i0];
+    const int nh = a.side[kk] ? h : jj, nt = a.side[kk] ? jj : t;
+    const T* eh = a.ent + (int64_t)h * a.ld;
+    const T* et = a.ent + (int64_t)t * a.ld;
+    const T* enh = a.ent + (int64_t)nh * a.ld;
+    const T* ent_ = a.ent + (int64_t)nt * a.ld;
+    const T* Wr = a.W + (int64_t)r * n * a.ld;
+    T ph[CH][kVec], pt[CH][kVec], pnh[CH][kVec], pnt[CH][kVec];
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) ph[c][k] = pt[c][k] = pnh[c][k] = pnt[c][k] = T(0);
+    for (int j = 0; j < n; ++j) {
+        const T hj = eh[j], tj = et[j], nhj = enh[j], ntj = ent_[j];
+        const T* wrow = Wr + (int64_t)j * a.ld;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int e = c * (kWave * kVec) + l * kVec;
+            if (e >= n) continue;
+            const T w0 = wrow[e], w1 = wrow[e + 1];  // ld even: pair stays in the row
+            ph[c][0] += w0 * hj; ph[c][1] += w1 * hj;
+            pt[c][0] += w0 * tj; pt[c][1] += w1 * tj;
+            pnh[c][0] += w0 * nhj; pnh[c][1] += w1 * nhj;
+            pnt[c][0] += w0 * ntj; pnt[c][1] += w1 * ntj;
+        }
+    }
+    RowReg<T, CH> R;
+    R.load(a.rel + (int64_t)r * a.ld, n);
+    T ep = T(0), en = T(0);
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            const int e = c * (kWave * kVec) + l * kVec + k;
+            if (e >= n) continue;
+            const T dp = pt[c][k] - ph[c][k] - R.v[c][k];
+            const T dn = pnt[c][k] - pnh[c][k] - R.v[c][k];
+            ep += a.l1 ? fabs(dp) : dp * dp;
+            en += a.l1 ? fabs(dn) : dn * dn;
+            T xp = T(2.0) * dp, xn = T(2.0) * dn;
+            if (a.l1) {
+                xp = xp > T(0) ? T(1) : T(-1);
+                xn = xn > T(0) ? T(1) : T(-1);
+            }
+            a.x[((int64_t)kk * 2 + 0) * a.ld + e] = xp;
+            a.x[((int64_t)kk * 2 + 1) * a.ld + e] = xn;
+            a.d[((int64_t)kk * 2 + 0) * a.ld + e] = eh[e] - et[e];
+            a.d[((int64_t)kk * 2 + 1) * a.ld + e] = enh[e] - ent_[e];
+            if (a.compat) {
+                double* pr = a.proj + ((int64_t)kk * 2 + 0) * 2 * a.ld;
+                pr[e] = (double)ph[c][k];
+                pr[a.ld + e] = (double)pt[c][k];
+                pr[2 * a.ld + e] = (double)pnh[c][k];
+                pr[3 * a.ld + e] = (double)pnt[c][k];
+            }
+        }
+    if (a.compat) return;  // energies come from the scanned work vectors
+    ep = wave_sum(ep);
+    en = wave_sum(en);
+    const double e_pos = (double)ep, e_neg = (double)en;
+    const bool active = e_pos + a.margin > e_neg;
+    if (l == 0) {
+        a.act[kk] = active ? 1 : 0;
+        a.loss[kk] = active ? a.margin + e_pos - e_neg : 0.0;
+    }
+}
+
+// Compat mode: the reference's work vectors accumulate every energy call's
+// projection and are never zeroed (transr/transr.cpp:20-25, trainer.h:28-29),
+// so call c sees hv = hv0 + sum_{c' <= c} W^T h_c'.  One wave per element i
+// scans the batch's 2B calls in order (pos before neg) and carries the
+// process-lifetime state in `work` ([2][n]: head, tail).
+__global__ __launch_bounds__(64) void transr_compat_scan_kernel(double* proj, int32_t B, int32_t ld, int32_t n,
+                                                                double* work) {
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    const int l = lane_id();
+    const int64_t calls = 2ll * B;
+    const int64_t per = (calls + kWave - 1) / kWave;
+    const int64_t c0 = l * per, c1 = min<int64_t>(calls, c0 + per);
+    double sh = 0, st = 0;
+    for (int64_t c = c0; c < c1; ++c) {
+        sh += proj[c * 2 * ld + i];
+        st += proj[(c * 2 + 1) * ld + i];
+    }
+    // exclusive scan of the lane sums (in lane order)
+    double eh = sh, et = st;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const double yh = __shfl_up(eh, off, 64), yt = __shfl_up(et, off, 64);
+        if (l >= off) {
+            eh += yh;
+            et += yt;
+        }
+    }
+    double rh = work[i] + (eh - sh), rt = work[n + i] + (et - st);
+    for (int64_t c = c0; c < c1; ++c) {
+        rh += proj[c * 2 * ld + i];
+        rt += proj[(c * 2 + 1) * ld + i];
+        proj[c * 2 * ld + i] = rh;
+        proj[(c * 2 + 1) * ld + i] = rt;
+    }
+    if (l == kWave - 1) {
+        work[i] = rh;
+        work[n + i] = rt;
+    }
+}
+
+template <typename T, int CH>
+__global__ __launch_bounds__(256) void transr_compat_energy_kernel(RScoreArgs<T> a) {
+    const int kk = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (kk >= a.B) return;
+    const int l = lane_id();
+    const int r = a.rels[a.si[kk]];
+    RowReg<T, CH> R;
+    R.load(a.rel + (int64_t)r * a.ld, a.n);
+    const double* pp = a.proj + ((int64_t)kk * 2 + 0) * 2 * a.ld;
+    double ep = 0, en = 0;
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            const int e = c * (kWave * kVec) + l * kVec + k;
+            if (e >= a.n) continue;
+            const double dp = pp[a.ld + e] - pp[e] - (double)R.v[c][k];
+            const double dn = pp[3 * a.ld + e] - pp[2 * a.ld + e] - (double)R.v[c][k];
+            ep += a.l1 ? fabs(dp) : dp * dp;
+            en += a.l1 ? fabs(dn) : dn * dn;
+        }
+    ep = wave_sum(ep);
+    en = wave_sum(en);
+    const bool active = ep + a.margin > en;
+    if (l == 0) {
+        a.act[kk] = active ? 1 : 0;
+        a.loss[kk] = active ? a.margin + ep - en : 0.0;
+    }
+}
+
+// ---------------------------------------------------------- TransR phase B
+
+// transRNorm (transr/trainer.cpp:35-64) on an entity row held in registers,
+// with the relation matrix W (n x ldl) in LDS and `abuf` (n) as broadcast
+// scratch.  Sums over j run in the reference's order for the check; the
+// per-column dot products of the iteration use the wave reduction.
+template <typename T, int CH>
+__device__ void transr_norm(RowReg<T, CH>& A, T* Wl, int ldl, T* abuf, int n, T lr) {
+    const int l = lane_id();
+    for (int iter = 0; iter < 100000; ++iter) {
+        A.store(abuf, n);
+        __syncthreads();
+        T xx = T(0);
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) {
+                const int i = c * (kWave * kVec) + l * kVec + k;
+                if (i >= n) continue;
+                T tmp = T(0);
+                for (int j = 0; j < n; ++j) tmp += Wl[j * ldl + i] * abuf[j];
+                xx += tmp * tmp;
+            }
+        xx = wave_sum(xx);
+        __syncthreads();
+        if (xx <= T(1)) break;
+        const T lambda = T(1);
+        for (int i = 0; i < n; ++i) {
+            T part = T(0);
+#pragma unroll
+            for (int c = 0; c < CH; ++c)
+#pragma unroll
+                for (int k = 0; k < kVec; ++k) {
+                    const int j = c * (kWave * kVec) + l * kVec + k;
+                    if (j < n) part += Wl[j * ldl + i] * A.v[c][k];
+                }
+            T tmp = wave_sum(part);
+            tmp *= T(2);
+            const T coef = lr * lambda * tmp;
+#pragma unroll
+            for (int c = 0; c < CH; ++c)
+#pragma unroll
+                for (int k = 0; k < kVec; ++k) {
+                    const int j = c * (kWave * kVec) + l * kVec + k;
+                    if (j >= n) continue;
+                    const T wn = Wl[j * ldl + i] - coef * A.v[c][k];
+                    Wl[j * ldl + i] = wn;
+                    A.v[c][k] = A.v[c][k] - coef * wn;
+                }
+            __syncthreads();
+        }
+    }
+}
+
+template <typename T>
+__device__ void w_spill(const T* Wl, int ldl, T* Wg, int n, int ld) {
+    for (int idx = lane_id(); idx < n * n; idx += kWave) {
+        const int j = idx / n, i = idx % n;
+        Wg[(int64_t)j * ld + i] = Wl[j * ldl + i];
+    }
+}
+
+template <typename T>
+__device__ void w_fill(T* Wl, int ldl, const T* Wg, int n, int ld) {
+    for (int idx = lane_id(); idx < n * n; idx += kWave) {
+        const int j = idx / n, i = idx % n;
+        Wl[j * ldl + i] = Wg[(int64_t)j * ld + i];
+    }
+}
+
+template <typename T, int CH>
+__global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32_t stamp) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int seg = a.owner_seg[(int64_t)a.batch * a.owners + blockIdx.x];
+    if (seg < 0) return;
+    const int p0 = a.seg_start[seg], p1 = a.seg_start[seg + 1];
+    const int n = a.n;
+    const int ldl = n + 1;
+    T* Wl = (T*)smem;                    // n x ldl: the owner's relation matrix (next)
+    T* abuf = Wl + n * ldl;              // n: broadcast scratch
+    T* xb = abuf + n;                    // n: update direction
+    T* db = xb + n;                      // n: snapshot head - tail
+    const int l = lane_id();
+    const T lr = (T)a.lr;
+    int cur = -1;
+    for (int p = p0; p < p1; ++p) {
+        const uint64_t key = a.keys[p];
+        const int kk = a.kl.kk_of(key);
+        if (!a.act[kk]) continue;
+        const UpdateIds d = decode_update(a, key, true);
+        if (d.r != cur) {
+            __syncthreads();
+            if (cur >= 0) {
+                w_spill(Wl, ldl, a.w + (int64_t)cur * n * a.ld, n, a.ld);
+                if (l == 0) a.wtouched[cur] = stamp;
+            }
+            w_fill(Wl, ldl, a.w + (int64_t)d.r * n * a.ld, n, a.ld);
+            cur = d.r;
+            __syncthreads();
+        }
+        for (int q = 0; q < d.count; ++q) wait_ticket(a.done, d.ent[q], d.tick[q], a.err);
+        // slots: head is slot 0; tail/entrel slots by identity
+        int tslot = 0, eslot = 0;
+        for (int q = 0; q < d.count; ++q) {
+            if (d.roles[q] & kRoleTail) tslot = q;
+            if (d.roles[q] & kRoleEntRel) eslot = q;
+        }
+        RowReg<T, CH> E[3];
+        for (int q = 0; q < d.count; ++q) row_load_sc1(E[q], a.ent + (int64_t)d.ent[q] * a.ld, n);
+        RowReg<T, CH> R;
+        R.load(a.rel + (int64_t)d.r * a.ld, n);
+        const T* xg = a.xreal + ((int64_t)kk * 2 + d.u) * a.ld;
+        const T* dg = a.scal + ((int64_t)kk * 2 + d.u) * a.ld;
+        for (int i = l; i < n; i += kWave) {
+            xb[i] = xg[i];
+            db[i] = dg[i];
+        }
+        __syncthreads();
+        const T beta = d.u ? T(1) : T(-1);
+        const T blr = beta * lr;
+        // rank-1 update of W' (transr/trainer.cpp:167): W'[j][i] -= (blr x_i) d_j
+        for (int idx = l; idx < n * n; idx += kWave) {
+            const int j = idx / n, i = idx % n;
+            Wl[j * ldl + i] = Wl[j * ldl + i] - (blr * xb[i]) * db[j];
+        }
+        // entity deltas with the snapshot matrix, summed over i in order (:168-169)
+        const T* Ws = a.wsnap + (int64_t)d.r * n * a.ld;
+        const bool same = tslot == 0;
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) {
+                const int j = c * (kWave * kVec) + l * kVec + k;
+                if (j >= n) continue;
+                const T* wrow = Ws + (int64_t)j * a.ld;
+                T hv = E[0].v[c][k];
+                T tv = E[tslot].v[c][k];
+                for (int i = 0; i < n; ++i) {
+                    const T g = (blr * xb[i]) * wrow[i];
+                    if (same) {
+                        hv = hv - g;
+                        hv = hv + g;
+                    } else {
+                        hv = hv - g;
+                        tv = tv + g;
+                    }
+                }
+                E[0].v[c][k] = hv;
+                if (!same) E[tslot].v[c][k] = tv;
+            }
+        // relation (:171)
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) {
+                const int i = c * (kWave * kVec) + l * kVec + k;
+                if (i < n) R.v[c][k] = R.v[c][k] - blr * xb[i];
+            }
+        __syncthreads();
+        // unit norms (:174-180): r', h', t', then every row of W'
+        R.norm(n, false);
+        E[0].norm(n, false);
+        E[tslot].norm(n, false);
+        for (int j = l; j < n; j += kWave) {  // one lane per row: the reference's serial sum
+            T s = T(0);
+            for (int i = 0; i < n; ++i) s += Wl[j * ldl + i] * Wl[j * ldl + i];
+            const T len = sqrt(s);
+            for (int i = 0; i < n; ++i) Wl[j * ldl + i] = Wl[j * ldl + i] / len;
+        }
+        __syncthreads();
+        // transRNorm on head, tail and entity[relation] (:185-187)
+        transr_norm(E[0], Wl, ldl, abuf, n, lr);
+        transr_norm(E[tslot], Wl, ldl, abuf, n, lr);
+        transr_norm(E[eslot], Wl, ldl, abuf, n, lr);
+        R.store(a.rel + (int64_t)d.r * a.ld, n);
+        for (int q = 0; q < d.count; ++q) row_store_sc1(E[q], a.ent + (int64_t)d.ent[q] * a.ld, n);
+        drain_stores();
+        for (int q = 0; q < d.count; ++q) release_ticket(a.done, d.ent[q], d.tick[q]);
+    }
+    __syncthreads();
+    if (cur >= 0) {
+        w_spill(Wl, ldl, a.w + (int64_t)cur * n * a.ld, n, a.ld);
+        if (l == 0) a.wtouched[cur] = stamp;
+    }
+}
+
+// After phase B: the committed matrices (snapshot table) take the new values
+// of every relation touched in this batch.
+template <typename T>
+__global__ __launch_bounds__(256) void transr_commit_kernel(const T* wnext, T* wsnap, const uint32_t* touched,
+                                                            uint32_t stamp, int32_t nr, int32_t n, int32_t ld) {
+    const int64_t rows = (int64_t)nr * n;
+    for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+        if (touched[row / n] != stamp) continue;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) wsnap[row * ld + i] = wnext[row * ld + i];
+    }
+}
 }  // namespace kb2e

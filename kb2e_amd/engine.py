@@ -21,7 +21,7 @@ SAMPLER_GLIBC, SAMPLER_REPLAY = 0, 1
 # Every symbol include/kb2e_engine.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "kb2e_default_config", "kb2e_create", "kb2e_destroy", "kb2e_last_error", "kb2e_upload_triples",
-    "kb2e_init_params", "kb2e_upload_params", "kb2e_download_params", "kb2e_get_transr_work",
+    "kb2e_init_params", "kb2e_transr_seed", "kb2e_upload_params", "kb2e_download_params", "kb2e_get_transr_work",
     "kb2e_set_transr_work", "kb2e_set_sample_stream", "kb2e_train_epoch", "kb2e_train_batches",
     "kb2e_synchronize", "kb2e_take_stats", "kb2e_rng_next", "kb2e_profile_enable", "kb2e_profile_query",
     "kb2e_device_bytes", "kb2e_device_tables", "kb2e_renormalize",
@@ -56,6 +56,7 @@ def lib():
             "kb2e_upload_triples": (i32, [vp, i32p, i32p, i32p, i64]),
             "kb2e_init_params": (i32, [vp, dp, dp, dp]),
             "kb2e_upload_params": (i32, [vp, dp, dp, dp]),
+            "kb2e_transr_seed": (i32, [vp, dp, dp]),
             "kb2e_download_params": (i32, [vp, dp, dp, dp]),
             "kb2e_get_transr_work": (i32, [vp, dp, dp]),
             "kb2e_set_transr_work": (i32, [vp, dp, dp]),
@@ -140,6 +141,11 @@ class Engine:
         w = np.zeros(self.wshape()) if self.wshape() else None
         self._check(lib().kb2e_init_params(self.h, _dp(ent), _dp(rel), _dp(w)), "init_params")
         return ent, rel, w
+
+    def transr_seed(self, ent, rel):
+        ent = np.ascontiguousarray(ent, dtype=np.float64)
+        rel = np.ascontiguousarray(rel, dtype=np.float64)
+        self._check(lib().kb2e_transr_seed(self.h, _dp(ent), _dp(rel)), "transr_seed")
 
     def upload_params(self, ent, rel, w=None):
         ent = np.ascontiguousarray(ent, dtype=np.float64)

@@ -1,0 +1,93 @@
+"""TransR on the GPU (relation-owner dataflow, matrices in LDS) vs the reference.
+
+Parity bar: FP64 engine within 1e-11 (golden runs: 2 epochs of the tiny set)
+or 1e-9 (multi-epoch coupled oracle runs, see gpu_common.F64_ATOL_COUPLED) of
+the FP64 reference tables -- entities, relations and every relation matrix --
+with identical hinge-active counts.  Both the reference's accumulating energy
+(compat, transr/transr.cpp:20-25) and the zeroed energy (fixed) are covered;
+transRNorm (transr/trainer.cpp:35-64) must iterate in the runs being matched.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from gpu_common import F64_ATOL, F64_ATOL_COUPLED, golden_engine, max_abs, oracle_model
+from kb2e_amd import data
+from kb2e_amd.engine import Engine
+from oracle import orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["transr_compat", "transr_fixed"])
+def test_golden_training_run_fp64(name):
+    eng, run, ds, _ = golden_engine(name)
+    d = os.path.join(GOLDEN, name)
+    e, r, w = eng.download_params()
+    assert np.array_equal(w, np.load(os.path.join(d, "init_w.npy")))
+    losses = np.load(os.path.join(d, "epoch_loss.npy"))
+    actives = np.load(os.path.join(d, "epoch_active.npy"))
+    for ep in range(run["flags"]["epochs"]):
+        loss, act = eng.train_epoch()
+        assert act == actives[ep], (ep, act, actives[ep])
+        assert abs(loss - losses[ep]) <= 1e-9 * max(1.0, abs(losses[ep])), (loss, losses[ep])
+        e, r, w = eng.download_params()
+        err = max(max_abs(e, np.load(os.path.join(d, f"epoch{ep}_ent.npy"))),
+                  max_abs(r, np.load(os.path.join(d, f"epoch{ep}_rel.npy"))),
+                  max_abs(w, np.load(os.path.join(d, f"epoch{ep}_w.npy"))))
+        assert err < F64_ATOL, (ep, err)
+    if name == "transr_compat":
+        hw, tw = eng.transr_work()
+        assert max_abs(hw, np.load(os.path.join(d, "epoch1_hwork.npy"))) < 1e-6 * max(1, np.abs(hw).max())
+    after = np.load(os.path.join(d, "rand_after.npy"))
+    assert [eng.rng_next() for _ in range(after.size)] == after.tolist()
+
+
+@pytest.mark.parametrize("compat,dim", [(False, 32), (True, 20), (False, 50)])
+def test_oracle_parity_with_transrnorm(compat, dim):
+    ds = data.synthetic("small", seed=4)
+    kw = dict(rate=0.005, margin=1.0, method=1, batches=25)
+    m = oracle_model("R", ds, dim, transr_compat=compat, **kw)
+    orc.srand(8)
+    m.prep_train()
+    eng = Engine("R", dim, ds.num_entities, ds.num_relations, seed=8, transr_compat=compat, **kw)
+    eng.upload_triples(ds.train)
+    e0, r0, w0 = eng.init_params()
+    # seed with the init draws themselves (the oracle's transr_seed applies the same unit norm)
+    m.transr_seed(e0, r0)
+    eng.transr_seed(e0, r0)
+    ge, gr, gw = eng.download_params()
+    oe, orl, ow = m.tables()
+    assert np.array_equal(ge, oe) and np.array_equal(gr, orl) and np.array_equal(gw, ow)
+    L = orc.lib()
+    before = [L.orc_site_iterations(s) for s in range(3)]
+    for ep in range(2):
+        lo, ao = m.train_epoch()
+        lg, ag = eng.train_epoch()
+        assert ag == ao, (ep, ag, ao)
+        assert abs(lg - lo) <= 1e-8 * max(1.0, abs(lo)), (lg, lo)
+        ge, gr, gw = eng.download_params()
+        oe, orl, ow = m.tables()
+        err = max(max_abs(ge, oe), max_abs(gr, orl), max_abs(gw, ow))
+        assert err < F64_ATOL_COUPLED, (ep, err)
+    assert sum(L.orc_site_iterations(s) - before[s] for s in range(3)) > 0
+
+
+def test_fp32_close_after_one_epoch():
+    ds = data.synthetic("small", seed=6)
+    kw = dict(rate=0.005, batches=25, transr_compat=False)
+    m = oracle_model("R", ds, 32, **kw)
+    orc.srand(3)
+    m.prep_train()
+    eng = Engine("R", 32, ds.num_entities, ds.num_relations, seed=3, precision=32, **kw)
+    eng.upload_triples(ds.train)
+    e0, r0, _ = eng.init_params()
+    m.transr_seed(e0, r0)
+    eng.transr_seed(e0, r0)
+    m.train_epoch()
+    eng.train_epoch()
+    ge, gr, gw = eng.download_params()
+    oe, orl, ow = m.tables()
+    assert max(max_abs(ge, oe), max_abs(gr, orl), max_abs(gw, ow)) < 1e-3
