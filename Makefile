@@ -8,7 +8,17 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -Wall 
 
 CSRC := $(wildcard kb2e_amd/csrc/*.hip kb2e_amd/csrc/*.hpp kb2e_amd/csrc/*.inc) include/kb2e_engine.h
 
-all: kb2e_amd/libkb2e.so oracle
+BINS := bin/trainTransE bin/trainTransH bin/trainTransR bin/evalTransE bin/evalTransH bin/evalTransR
+
+all: kb2e_amd/libkb2e.so bin/kb2e $(BINS) oracle
+
+bin/kb2e: kb2e_amd/csrc/host/kb2e_cli.cpp include/kb2e_engine.h kb2e_amd/libkb2e.so
+	@mkdir -p bin
+	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ kb2e_amd/csrc/host/kb2e_cli.cpp -Lkb2e_amd -lkb2e \
+	    -Wl,-rpath,'$$ORIGIN/../kb2e_amd'
+
+$(BINS): bin/kb2e
+	ln -sf kb2e $@
 
 kb2e_amd/libkb2e.so: $(CSRC)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ kb2e_amd/csrc/engine.hip
@@ -20,7 +30,7 @@ ref:
 	$(MAKE) -C oracle ref
 
 clean:
-	rm -f kb2e_amd/libkb2e.so
+	rm -f kb2e_amd/libkb2e.so bin/kb2e $(BINS)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle ref clean

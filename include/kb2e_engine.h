@@ -111,6 +111,10 @@ kb2e_status kb2e_set_transr_work(kb2e_ctx* ctx, const double* head_work, const d
 kb2e_status kb2e_set_sample_stream(kb2e_ctx* ctx, const int32_t* i, const int32_t* j,
                                    const uint8_t* side, int64_t count);
 
+/* The sample stream of the epoch in progress (after its first batch was
+ * queued): up to `count` samples in order.  Returns KB2E_ESTATE between epochs. */
+kb2e_status kb2e_get_sample_stream(kb2e_ctx* ctx, int32_t* i, int32_t* j, uint8_t* side, int64_t count);
+
 /* One epoch of Trainer::bfgs (common/trainer.cpp:72-106): numBatches batches of
  * floor(|train| / numBatches) samples.  *loss = the epoch loss the reference
  * prints at :105; *active = hinge-active samples.  Either pointer may be NULL. */
@@ -123,6 +127,19 @@ kb2e_status kb2e_train_batches(kb2e_ctx* ctx, int32_t nbatches);
 kb2e_status kb2e_synchronize(kb2e_ctx* ctx);
 /* Loss and active count accumulated since the last call (resets them). */
 kb2e_status kb2e_take_stats(kb2e_ctx* ctx, double* loss, int64_t* active);
+
+/* Link prediction on the current device tables (EmbeddingEvaluation::run,
+ * common/evaluation.cpp:181-251): for each test triple, corrupt the head and
+ * the tail with every entity, rank the true triple by energy; filtered ranks
+ * skip corruptions that are in the filter set (the reference passes test +
+ * train + valid, common/evaluation.cpp:41-62).  out[0..3] = raw mean rank,
+ * raw hits@10, filtered mean rank, filtered hits@10 (hits as fractions, as
+ * printed at :249-250).  Energies are bit-identical FP64 restatements of the
+ * reference's; ties with the true triple are not counted above it.  TransR
+ * uses the zeroed (fixed) work vectors.  Requires dim <= 128. */
+kb2e_status kb2e_evaluate(kb2e_ctx* ctx, const int32_t* heads, const int32_t* tails, const int32_t* relations,
+                          int64_t ntest, const int32_t* filter_heads, const int32_t* filter_tails,
+                          const int32_t* filter_relations, int64_t nfilter, double* out);
 
 /* Raw glibc stream access (the context's RNG, as std::rand() in the reference). */
 int32_t kb2e_rng_next(kb2e_ctx* ctx);

@@ -31,6 +31,7 @@
 #include "kernels_transe.hpp"
 #include "kernels_relowner.hpp"
 #include "kernels_sampler.hpp"
+#include "kernels_eval.hpp"
 
 using namespace kb2e;
 
@@ -773,6 +774,7 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
         const char* hs = getenv("KB2E_HOST_SAMPLER");
         c->host_sampler = hs && hs[0] == '1';
         setup_buffers(c.get());
+        HIPCHK(hipDeviceSynchronize());
         return KB2E_OK;
     });
     if (s != KB2E_OK) return s;
@@ -808,6 +810,9 @@ kb2e_status kb2e_upload_triples(kb2e_ctx* c, const int32_t* h, const int32_t* t,
         HIPCHK(hipMemcpy(c->pr_dev.p, pr.data(), pr.size() * 8, hipMemcpyHostToDevice));
         if (c->cfg.model != KB2E_TRANSE) plan_owners(c->plan, c->ts, c->cfg.num_relations, c->num_cus);
         setup_epoch_buffers(c);
+        // setup used the legacy stream (hipMemset/hipMemcpy): the non-blocking
+        // engine stream does not order against it, so drain it here
+        HIPCHK(hipDeviceSynchronize());
         c->have_triples = true;
         c->epoch_pos = 0;
         c->epoch_ready = false;
@@ -930,6 +935,7 @@ kb2e_status kb2e_set_transr_work(kb2e_ctx* c, const double* hw, const double* tw
         std::vector<double> h(2 * (size_t)c->n);
         std::memcpy(h.data(), hw, (size_t)c->n * 8);
         std::memcpy(h.data() + c->n, tw, (size_t)c->n * 8);
+        HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipMemcpy(c->transr_work.p, h.data(), h.size() * 8, hipMemcpyHostToDevice));
         return KB2E_OK;
     });
@@ -946,6 +952,18 @@ kb2e_status kb2e_set_sample_stream(kb2e_ctx* c, const int32_t* i, const int32_t*
         c->rp_sj.assign(j, j + count);
         c->rp_side.assign(side, side + count);
         c->rp_pos = 0;
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_get_sample_stream(kb2e_ctx* c, int32_t* i, int32_t* j, uint8_t* side, int64_t count) {
+    return guarded(c, [&] {
+        if (!c->epoch_ready) return fail(c, KB2E_ESTATE, "no epoch in progress");
+        const int64_t k = std::min<int64_t>(count, c->S);
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipMemcpy(i, c->si(), k * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(j, c->sj(), k * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(side, c->side(), k, hipMemcpyDeviceToHost));
         return KB2E_OK;
     });
 }
@@ -990,6 +1008,117 @@ kb2e_status kb2e_train_epoch(kb2e_ctx* c, double* loss, int64_t* active) {
         if (active) *active = c->acc_active;
         c->acc_loss = 0;
         c->acc_active = 0;
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_evaluate(kb2e_ctx* c, const int32_t* th, const int32_t* tt, const int32_t* tr, int64_t ntest,
+                          const int32_t* fh, const int32_t* ft, const int32_t* fr, int64_t nfilter, double* out) {
+    return guarded(c, [&] {
+        if (!th || !tt || !tr || ntest < 1 || !out) return fail(c, KB2E_EINVAL, "empty test set");
+        if (c->n > 128) return fail(c, KB2E_EUNSUPPORTED, "evaluation supports dim <= 128");
+        if (!c->have_params) return fail(c, KB2E_ESTATE, "no embeddings on the device");
+        HIPCHK(hipSetDevice(c->cfg.device));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        const int ne = c->cfg.num_entities, nr = c->cfg.num_relations, n = c->n;
+        // filter set (test + train + valid in the caller's order; duplicates are fine)
+        std::vector<int32_t> H(fh, fh + nfilter), T(ft, ft + nfilter), R(fr, fr + nfilter);
+        for (int64_t k = 0; k < nfilter; ++k)
+            if (H[k] < 0 || H[k] >= ne || T[k] < 0 || T[k] >= ne || R[k] < 0 || R[k] >= nr)
+                return fail(c, KB2E_EINVAL, "filter triple out of range");
+        FilterSet fs;
+        fs.build(H, T, R, ne, nr);
+        // test triples grouped by relation (the reference visits relations in id order)
+        std::vector<std::vector<int64_t>> byrel(nr);
+        for (int64_t k = 0; k < ntest; ++k) {
+            if (th[k] < 0 || th[k] >= ne || tt[k] < 0 || tt[k] >= ne || tr[k] < 0 || tr[k] >= nr)
+                return fail(c, KB2E_EINVAL, "test triple out of range");
+            byrel[tr[k]].push_back(k);
+        }
+        std::vector<int32_t> qh, qt;
+        std::vector<int64_t> qoff(nr + 1, 0);
+        for (int r = 0; r < nr; ++r) {
+            for (int64_t k : byrel[r]) {
+                qh.push_back(th[k]);
+                qt.push_back(tt[k]);
+            }
+            qoff[r + 1] = (int64_t)qh.size();
+        }
+        DevBuf d_slots, d_qh, d_qt, d_counts, d_target, d_PT, d_relv;
+        d_slots.alloc(fs.slots.size() * 8);
+        HIPCHK(hipMemcpy(d_slots.p, fs.slots.data(), fs.slots.size() * 8, hipMemcpyHostToDevice));
+        d_qh.alloc(qh.size() * 4);
+        d_qt.alloc(qt.size() * 4);
+        HIPCHK(hipMemcpy(d_qh.p, qh.data(), qh.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(d_qt.p, qt.data(), qt.size() * 4, hipMemcpyHostToDevice));
+        d_counts.alloc(qh.size() * 4 * 8);
+        HIPCHK(hipMemset(d_counts.p, 0, d_counts.bytes));
+        d_target.alloc(qh.size() * 2 * 8);
+        d_PT.alloc((size_t)n * ne * 8);
+        d_relv.alloc((size_t)n * 8);
+        HIPCHK(hipDeviceSynchronize());  // legacy-stream memset/copies above vs the engine stream
+        for (int r = 0; r < nr; ++r) {
+            const int64_t nq = qoff[r + 1] - qoff[r];
+            if (nq == 0) continue;
+            c->timed("eval", [&] {
+                const int pg = (std::max(ne, n) + 255) / 256;
+                if (c->f64()) {
+                    EvalArgs<double> ea{c->cfg.model, n, c->ld, ne, c->cfg.distance == 0 || c->cfg.model == KB2E_TRANSH,
+                                        c->ent.as<double>(), c->rel.as<double>(),
+                                        c->cfg.model == KB2E_TRANSR ? c->wsnap.as<double>() : c->w.as<double>(), r,
+                                        d_PT.as<double>(), d_relv.as<double>()};
+                    eval_project_kernel<double><<<pg, 256, 0, c->stream>>>(ea);
+                } else {
+                    EvalArgs<float> ea{c->cfg.model, n, c->ld, ne, c->cfg.distance == 0 || c->cfg.model == KB2E_TRANSH,
+                                       c->ent.as<float>(), c->rel.as<float>(),
+                                       c->cfg.model == KB2E_TRANSR ? c->wsnap.as<float>() : c->w.as<float>(), r,
+                                       d_PT.as<double>(), d_relv.as<double>()};
+                    eval_project_kernel<float><<<pg, 256, 0, c->stream>>>(ea);
+                }
+                HIPCHK(hipGetLastError());
+                RankArgs ra{};
+                ra.PT = d_PT.as<double>();
+                ra.relv = d_relv.as<double>();
+                ra.n = n;
+                ra.ne = ne;
+                ra.l1 = c->cfg.distance == 0 || c->cfg.model == KB2E_TRANSH;
+                ra.r = r;
+                ra.qh = d_qh.as<int32_t>() + qoff[r];
+                ra.qt = d_qt.as<int32_t>() + qoff[r];
+                ra.nq = (int32_t)nq;
+                ra.slots = d_slots.as<uint64_t>();
+                ra.mask = fs.mask;
+                ra.nr64 = (uint64_t)nr;
+                ra.ne64 = (uint64_t)ne;
+                ra.counts = d_counts.as<unsigned long long>() + qoff[r] * 4;
+                ra.target = d_target.as<double>() + qoff[r] * 2;
+                eval_target_kernel<<<(int)((nq + 255) / 256), 256, 0, c->stream>>>(ra);
+                HIPCHK(hipGetLastError());
+                dim3 grid((ne + 255) / 256, (unsigned)((nq + kQ - 1) / kQ));
+                eval_rank_kernel<<<grid, 256, 0, c->stream>>>(ra);
+                HIPCHK(hipGetLastError());
+            });
+        }
+        // the engine stream is non-blocking: wait for it before reading back
+        HIPCHK(hipStreamSynchronize(c->stream));
+        std::vector<unsigned long long> counts(qh.size() * 4);
+        HIPCHK(hipMemcpy(counts.data(), d_counts.p, counts.size() * 8, hipMemcpyDeviceToHost));
+        long long rawSum = 0, filtSum = 0, rawHits = 0, filtHits = 0;
+        for (size_t q = 0; q < qh.size(); ++q) {
+            for (int side = 0; side < 2; ++side) {
+                const long long raw = 1 + (long long)counts[q * 4 + 2 * side];
+                const long long filt = 1 + (long long)counts[q * 4 + 2 * side + 1];
+                rawSum += raw;
+                filtSum += filt;
+                rawHits += raw <= 10;
+                filtHits += filt <= 10;
+            }
+        }
+        const double nc = (double)ntest * 2.0;
+        out[0] = rawSum / nc;
+        out[1] = rawHits / nc;
+        out[2] = filtSum / nc;
+        out[3] = filtHits / nc;
         return KB2E_OK;
     });
 }

@@ -22,9 +22,9 @@ SAMPLER_GLIBC, SAMPLER_REPLAY = 0, 1
 EXPORTS = [
     "kb2e_default_config", "kb2e_create", "kb2e_destroy", "kb2e_last_error", "kb2e_upload_triples",
     "kb2e_init_params", "kb2e_transr_seed", "kb2e_upload_params", "kb2e_download_params", "kb2e_get_transr_work",
-    "kb2e_set_transr_work", "kb2e_set_sample_stream", "kb2e_train_epoch", "kb2e_train_batches",
+    "kb2e_set_transr_work", "kb2e_set_sample_stream", "kb2e_get_sample_stream", "kb2e_train_epoch", "kb2e_train_batches",
     "kb2e_synchronize", "kb2e_take_stats", "kb2e_rng_next", "kb2e_profile_enable", "kb2e_profile_query",
-    "kb2e_device_bytes", "kb2e_device_tables", "kb2e_renormalize",
+    "kb2e_device_bytes", "kb2e_device_tables", "kb2e_renormalize", "kb2e_evaluate",
 ]
 
 
@@ -61,6 +61,7 @@ def lib():
             "kb2e_get_transr_work": (i32, [vp, dp, dp]),
             "kb2e_set_transr_work": (i32, [vp, dp, dp]),
             "kb2e_set_sample_stream": (i32, [vp, i32p, i32p, u8p, i64]),
+            "kb2e_get_sample_stream": (i32, [vp, i32p, i32p, u8p, i64]),
             "kb2e_train_epoch": (i32, [vp, dp, C.POINTER(i64)]),
             "kb2e_train_batches": (i32, [vp, i32]),
             "kb2e_synchronize": (i32, [vp]),
@@ -72,6 +73,7 @@ def lib():
             "kb2e_device_tables": (i32, [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(i64),
                                          C.POINTER(i64), C.POINTER(i64)]),
             "kb2e_renormalize": (i32, [vp, u8p, u8p, u8p]),
+            "kb2e_evaluate": (i32, [vp, i32p, i32p, i32p, i64, i32p, i32p, i32p, i64, dp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -179,6 +181,14 @@ class Engine:
                                                  side.ctypes.data_as(C.POINTER(C.c_uint8)), len(si)),
                     "set_sample_stream")
 
+    def sample_stream(self, count):
+        si = np.zeros(count, np.int32)
+        sj = np.zeros(count, np.int32)
+        side = np.zeros(count, np.uint8)
+        self._check(lib().kb2e_get_sample_stream(self.h, _ip(si), _ip(sj), side.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                                 count), "get_sample_stream")
+        return si, sj, side
+
     def train_epoch(self):
         loss = C.c_double(0)
         act = C.c_int64(0)
@@ -213,6 +223,17 @@ class Engine:
         keep = [None if m is None else np.ascontiguousarray(m, dtype=np.uint8) for m in (ent_rows, rel_rows, w_rows)]
         ptrs = [None if m is None else m.ctypes.data_as(C.POINTER(C.c_uint8)) for m in keep]
         self._check(lib().kb2e_renormalize(self.h, *ptrs), "renormalize")
+
+    def evaluate(self, test, filt):
+        """Link prediction (raw/filtered mean rank and hits@10) on the device tables."""
+        test = np.ascontiguousarray(test, dtype=np.int32)
+        filt = np.ascontiguousarray(filt, dtype=np.int32)
+        tc = [np.ascontiguousarray(test[:, k]) for k in range(3)]
+        fc = [np.ascontiguousarray(filt[:, k]) for k in range(3)]
+        out = np.zeros(4)
+        self._check(lib().kb2e_evaluate(self.h, _ip(tc[0]), _ip(tc[1]), _ip(tc[2]), len(test), _ip(fc[0]),
+                                        _ip(fc[1]), _ip(fc[2]), len(filt), _dp(out)), "evaluate")
+        return {"raw_rank": out[0], "raw_hits10": out[1], "filtered_rank": out[2], "filtered_hits10": out[3]}
 
     def device_bytes(self):
         return lib().kb2e_device_bytes(self.h)

@@ -3,6 +3,7 @@
  * TEST INFRASTRUCTURE ONLY (see orc.h).  Compiled with -ffp-contract=off so
  * every multiply/add rounds exactly as the reference's x86-64 SSE2 build does.
  */
+#define _DEFAULT_SOURCE
 #include "orc.h"
 
 #include <math.h>
@@ -33,6 +34,14 @@ struct orc_model {
     double *hwork, *twork;
 };
 
+/* The reference's RNG is glibc rand() (TYPE_3 random_r on a global state).
+ * The oracle keeps a PRIVATE TYPE_3 state and draws with random_r: the same
+ * algorithm and stream, but immune to other rand() callers in the process
+ * (the HIP runtime draws from the global state while it initialises). */
+static struct random_data g_rd;
+static char g_rstate[128];  /* 128 bytes selects TYPE_3, glibc's rand() default */
+static int g_rinit = 0;
+
 static long long g_orth_iters = 0;
 static long long g_site_iters[4];
 static int g_site = 3;
@@ -40,12 +49,25 @@ static long long g_transr_norm_iters = 0;
 
 /* ------------------------------------------------------------------ L0 */
 
-void orc_srand(unsigned seed) { srand(seed); }
-int orc_rand(void) { return rand(); }
+void orc_srand(unsigned seed) {
+    if (!g_rinit) {
+        memset(&g_rd, 0, sizeof(g_rd));
+        initstate_r(seed, g_rstate, sizeof(g_rstate), &g_rd);
+        g_rinit = 1;
+    }
+    srandom_r(seed, &g_rd);
+}
+
+int orc_rand(void) {
+    int32_t r;
+    if (!g_rinit) orc_srand(1); /* glibc: rand() without srand() behaves as srand(1) */
+    random_r(&g_rd, &r);
+    return (int)r;
+}
 
 /* common/utils.cpp:18-20 */
 double orc_rand_range(double min, double max) {
-    return min + (max - min) * rand() / (RAND_MAX + 1.0);
+    return min + (max - min) * orc_rand() / (RAND_MAX + 1.0);
 }
 
 static double sqr(double x) { return x * x; } /* common/utils.cpp:40-42 */
@@ -68,8 +90,8 @@ double orc_randn(double miu, double sigma, double min, double max) {
 
 /* common/utils.cpp:113-120: (rand()*rand()) % x in int32 with wrap-around. */
 int orc_randmax(int x) {
-    unsigned a = (unsigned)rand();
-    unsigned b = (unsigned)rand();
+    unsigned a = (unsigned)orc_rand();
+    unsigned b = (unsigned)orc_rand();
     int res = (int)(a * b) % x;
     while (res < 0) res += x;
     return res;
@@ -539,7 +561,7 @@ static void draw_sample(orc_model* m, int* si, int* sj, int* side) {
     int r = m->rels[i];
     double pr = 1000 * m->tail_mean[r] / (m->tail_mean[r] + m->head_mean[r]);
     if (m->method == 0) pr = 500; /* METHOD_UNIF */
-    if (rand() % 1000 < pr) {
+    if (orc_rand() % 1000 < pr) {
         while (orc_in_train(m, m->heads[i], r, j)) j = orc_randmax(m->ne);
         *side = 1;
     } else {

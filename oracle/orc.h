@@ -13,8 +13,9 @@
  * path.  The product (kb2e_amd/csrc, libkb2e.so) does not link or call it.
  *
  * RNG: the reference draws from the global glibc rand() seeded by srand(seed)
- * in main() (transe/bin/trainTransE.cpp:13).  The oracle calls libc rand()
- * directly, so it is bit-identical to the reference on the same glibc.
+ * in main() (transe/bin/trainTransE.cpp:13).  The oracle draws the same TYPE_3
+ * stream through glibc's random_r on a private state, so it is bit-identical
+ * to the reference on the same glibc and unaffected by other rand() callers.
  */
 #ifndef KB2E_ORACLE_ORC_H_
 #define KB2E_ORACLE_ORC_H_

@@ -1,0 +1,86 @@
+"""Drop-in check: the trainTransE/H/R binaries (C++ host over the C ABI) run
+with the reference's flags on the reference's file formats and reproduce the
+reference binaries' stdout epoch lines and %.6lf embedding files."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+from gpu_common import MANIFEST
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(tmp_path, prog, name, extra=()):
+    run = MANIFEST["runs"][name]
+    exe = tmp_path / prog
+    if not exe.exists():
+        exe.symlink_to(os.path.join(ROOT, "bin", "kb2e"))
+    out = tmp_path / "out"
+    out.mkdir(exist_ok=True)
+    args = [str(exe), "--datadir", os.path.join(GOLDEN, "tiny"), "--outdir", str(out)]
+    for k, v in run["flags"].items():
+        args += ["--" + k, str(v)]
+    args += list(extra)
+    res = subprocess.run(args, capture_output=True, text=True, timeout=300, check=True)
+    return res.stdout, out, run
+
+
+def _epoch_lines(text):
+    return [l for l in text.splitlines() if l.startswith("Epoch:")]
+
+
+def _compare_files(out, name, files):
+    for f in files:
+        mine = np.array(open(out / f).read().split(), dtype=np.float64)
+        ref = np.array(open(os.path.join(GOLDEN, name, f)).read().split(), dtype=np.float64)
+        assert mine.shape == ref.shape
+        # identical text except where an ulp difference crosses a 1e-6 rounding boundary
+        assert np.abs(mine - ref).max() <= 1.000001e-6
+        assert (mine != ref).sum() <= 2
+
+
+def test_train_transe_cli(tmp_path):
+    stdout, out, run = _run(tmp_path, "trainTransE", "transe_l1_bern")
+    ref = open(os.path.join(GOLDEN, "transe_l1_bern", "stdout.txt")).read()
+    assert _epoch_lines(stdout) == _epoch_lines(ref)
+    assert "Number of Entities: 200" in stdout and "Options: [datadir:" in stdout
+    _compare_files(out, "transe_l1_bern", ["entity2vec.bern", "relation2vec.bern"])
+
+
+def test_train_transh_cli(tmp_path):
+    stdout, out, run = _run(tmp_path, "trainTransH", "transh_bern")
+    ref = open(os.path.join(GOLDEN, "transh_bern", "stdout.txt")).read()
+    assert _epoch_lines(stdout) == _epoch_lines(ref)
+    _compare_files(out, "transh_bern", ["entity2vec.bern", "relation2vec.bern", "weights.bern"])
+
+
+def test_train_transr_cli(tmp_path):
+    stdout, out, run = _run(tmp_path, "trainTransR", "transr_compat",
+                            ["--seeddatadir", os.path.join(GOLDEN, "transe_seed_unif")])
+    ref = open(os.path.join(GOLDEN, "transr_compat", "stdout.txt")).read()
+    assert _epoch_lines(stdout) == _epoch_lines(ref)
+    _compare_files(out, "transr_compat", ["entity2vec.bern", "relation2vec.bern", "weights.bern"])
+
+
+def test_missing_seed_file_fails_like_reference(tmp_path):
+    with pytest.raises(subprocess.CalledProcessError) as e:
+        _run(tmp_path, "trainTransR", "transr_compat", ["--seeddatadir", str(tmp_path / "nowhere")])
+    assert e.value.returncode == 1 and "Failed to read embedding values from seed file" in e.value.stdout
+
+
+def test_eval_cli_matches_reference_eval(tmp_path):
+    stdout, out, run = _run(tmp_path, "trainTransE", "transe_l1_bern")
+    exe = tmp_path / "evalTransE"
+    exe.symlink_to(os.path.join(ROOT, "bin", "kb2e"))
+    f = run["flags"]
+    res = subprocess.run([str(exe), "--datadir", os.path.join(GOLDEN, "tiny"), "--outdir",
+                          os.path.join(GOLDEN, "transe_l1_bern"), "--size", str(f["size"]), "--method",
+                          str(f["method"]), "--distance", str(f["distance"])],
+                         capture_output=True, text=True, timeout=300, check=True)
+    lines = {l.split("--")[0].strip(): l for l in res.stdout.splitlines() if "Hits@10" in l}
+    ev = run["eval"]
+    assert lines["Raw"] == "Raw      -- Rank: %f, Hits@10: %f" % (ev["raw"]["rank"], ev["raw"]["hits10"])
+    assert lines["Filtered"] == "Filtered -- Rank: %f, Hits@10: %f" % (ev["filtered"]["rank"], ev["filtered"]["hits10"])
