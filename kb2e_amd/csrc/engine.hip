@@ -145,6 +145,7 @@ struct kb2e_ctx {
     DevBuf owner, tickets, ent_done, wsnap, transr_work, owner_seg, dataflow_err, wtouched;
     int num_cus = 256;
     uint32_t batch_stamp = 0;
+    int32_t gram_min = 48;  // KB2E_GRAM_MIN: fold segments this long use the scalar recurrence (0 = off)
     // stats
     DevBuf stats;  // double loss, double active (reduced)
     double acc_loss = 0;
@@ -535,6 +536,7 @@ void run_batch_transe(kb2e_ctx* c, int64_t b) {
     fa.act = sa.act;
     fa.xbits = sa.xbits;
     fa.xreal = sa.xreal;
+    fa.gram_min = c->gram_min;
     // Enough waves for every touched row of a batch (<= 6 B segments).
     const int64_t max_seg = std::min<int64_t>(c->B * 6, (int64_t)c->cfg.num_entities + c->cfg.num_relations);
     const int fgrid = (int)std::max<int64_t>(1, std::min<int64_t>((max_seg + 3) / 4, 4096));
@@ -771,6 +773,7 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
         HIPCHK(hipEventRecord(c->ev_epoch_done, c->stream));
         HIPCHK(hipDeviceGetAttribute(&c->num_cus, hipDeviceAttributeMultiprocessorCount, g.device));
         prepare_relowner_kernels();
+        if (const char* gm = getenv("KB2E_GRAM_MIN")) c->gram_min = atoi(gm);
         const char* hs = getenv("KB2E_HOST_SAMPLER");
         c->host_sampler = hs && hs[0] == '1';
         setup_buffers(c.get());

@@ -56,6 +56,14 @@ __device__ __forceinline__ T wave_sum(T v) {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Order LDS traffic between the lanes of ONE wave (no workgroup barrier: the
+// other waves of the block may be elsewhere).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 // Read a wave-uniform 64-bit value held by lane `src` (src wave-uniform).
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int src) {
     uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, src);

@@ -119,10 +119,147 @@ struct FoldArgs {
     const uint8_t* act;     // [B] of this batch
     const uint64_t* xbits;  // [B][2][nw]
     const T* xreal;         // [B][2][ld]
+    int32_t gram_min;       // segments at least this long take the scalar-recurrence path (0: never)
 };
+
+// ---- long L1 segments: the renormalisation recurrence on scalars ----------
+//
+// A row's events are v <- v + e_k then "if |v| > 1: v /= |v|", with
+// e_k = s_k * lr * x_k, x_k in {+-1}^n (s_k = -1 relation / head role, +1 tail
+// role, 0 when the update uses the row as head AND tail, whose two deltas
+// cancel; transe/trainer.cpp:38-45).  Write v = A * u with
+// u = v0 + sum_j beta_j e_j (beta_j = 1/A when e_j was added).  Then
+//   |v + e_k|^2 = N + 2 A (v0.e_k + sum_{j<k} beta_j e_j.e_k) + |e_k|^2,
+// with N = |v|^2, and e_j.e_k = s_j s_k lr^2 (n - 2 popcount(bits_j ^ bits_k)).
+// Per chunk of 64 events: one reduction for N, 64 independent dot products
+// v0.e_m (lane m), a scalar chain (sqrt, reciprocal) per event while each lane
+// m accumulates S_m = sum_j beta_j e_j.e_m, and one elementwise
+// materialisation v = A (v0 + sum beta_j e_j).  Same decisions as the
+// reference; values agree to a few ulps per chunk.
+// 1/sqrt(x) to ~full FP64 precision: hardware estimate + two Newton steps.
+__device__ __forceinline__ double rsqrt_nr(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    y = y * (1.5 - 0.5 * x * y * y);
+    y = y * (1.5 - 0.5 * x * y * y);
+    return y;
+}
+
+template <typename T, int CH>
+__device__ void fold_segment_gram(const FoldArgs<T>& a, int p0, int p1, bool is_rel, RowReg<T, CH>& V,
+                                  double* lds_v, bool& dirty) {
+    const int l = lane_id();
+    const double lr = a.lr;
+    const double lr2 = lr * lr;
+    const double eps = lr2 * (double)a.n;
+    for (int base = p0; base < p1; base += kWave) {
+        const int cnt = min(kWave, p1 - base);
+        uint64_t xw[2 * CH];
+        int sgn = 0, nn = 0;
+#pragma unroll
+        for (int q = 0; q < 2 * CH; ++q) xw[q] = 0ull;
+        if (l < cnt) {
+            const uint64_t key = a.keys[base + l];
+            const int kk = a.kl.kk_of(key);
+            if (a.act[kk]) {
+                const int u = (int)((key >> 3) & 1);
+                const uint32_t roles = (uint32_t)(key & 7);
+                // e = s * lr * x: relation and head rows take -d, tail rows +d,
+                // d = (neg update ? +1 : -1) * lr * x (transe/trainer.cpp:26, 38-40)
+                const int us = u ? 1 : -1;
+                if (is_rel) {
+                    sgn = -us;
+                    nn = 1;
+                } else {
+                    const bool hd = roles & kRoleHead, tl = roles & kRoleTail;
+                    sgn = (hd && tl) ? 0 : (hd ? -us : us);
+                    nn = (hd ? 1 : 0) + (tl ? 1 : 0);
+                }
+#pragma unroll
+                for (int q = 0; q < 2 * CH; ++q) xw[q] = a.xbits[((int64_t)kk * 2 + u) * a.nw + q];
+            }
+        }
+        const uint64_t m_act = __ballot(nn > 0);
+        if (!m_act) continue;
+        const uint64_t m_sgn = __ballot(sgn != 0), m_n2 = __ballot(nn == 2);
+        dirty = true;
+        // p_m = s_m lr (v0 . x_m): v0 to LDS, lane m walks the row
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) {
+                const int e = c * (kWave * kVec) + l * kVec + k;
+                if (e < a.n) lds_v[e] = (double)V.v[c][k];
+            }
+        wave_lds_sync();
+        double pm = 0;
+        for (int e = 0; e < a.n; ++e) {
+            const int c = e / (kWave * kVec), r = e % (kWave * kVec);
+            const double v = lds_v[e];
+            pm += ((xw[c * kVec + (r & 1)] >> (r >> 1)) & 1ull) ? v : -v;
+        }
+        pm *= (double)sgn * lr;
+        // e_k . e_m / lr^2 = s_k s_m (n - 2 popcount(bits_k ^ bits_m)), for every k (lane m)
+        int gk[kWave];
+#pragma unroll
+        for (int k = 0; k < kWave; ++k) {
+            uint32_t dis = 0;
+#pragma unroll
+            for (int q = 0; q < 2 * CH; ++q) dis += (uint32_t)__popcll(xw[q] ^ readlane_u64(xw[q], k));
+            gk[k] = readlane_i32(sgn, k) * sgn * (a.n - 2 * (int)dis);
+        }
+        double N = (double)V.sumsq();
+        double A = 1.0, invA = 1.0, S = 0.0, beta_mine = 0.0;
+#pragma unroll
+        for (int k = 0; k < kWave; ++k) {
+            if (!((m_act >> k) & 1ull)) continue;  // wave-uniform
+            const double z2 = N + 2.0 * A * (readlane_f(pm, k) + readlane_f(S, k)) +
+                              (((m_sgn >> k) & 1ull) ? eps : 0.0);
+            beta_mine = (l == k) ? invA : beta_mine;
+            S += invA * lr2 * (double)gk[k];
+            double nz = z2;
+            if (z2 > 1.0) {  // common::norm: len > 1 -> v /= len
+                const double y = rsqrt_nr(z2);
+                A *= y;
+                invA *= z2 * y;
+                nz = z2 * y * y;
+            }
+            if (((m_n2 >> k) & 1ull) && nz > 1.0) {  // second role of the same row
+                const double y = rsqrt_nr(nz);
+                A *= y;
+                invA *= nz * y;
+                nz = nz * y * y;
+            }
+            N = nz;
+        }
+        // v = A * (v0 + sum_k beta_k s_k lr x_k)
+        double u[CH][kVec];
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) u[c][k] = (double)V.v[c][k];
+#pragma unroll
+        for (int k = 0; k < kWave; ++k) {
+            if (!((m_sgn >> k) & 1ull)) continue;
+            const double w = readlane_f(beta_mine, k) * (double)readlane_i32(sgn, k) * lr;
+            uint64_t words[2 * CH];
+#pragma unroll
+            for (int q = 0; q < 2 * CH; ++q) words[q] = readlane_u64(xw[q], k);
+#pragma unroll
+            for (int c = 0; c < CH; ++c)
+#pragma unroll
+                for (int kv = 0; kv < kVec; ++kv) u[c][kv] += xbit(words, c, kv) ? w : -w;
+        }
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) V.v[c][k] = elem_valid(c, k, a.n) ? (T)(A * u[c][k]) : T(0);
+        wave_lds_sync();
+    }
+}
 
 template <typename T, int CH, bool L1>
 __global__ __launch_bounds__(256) void transe_fold_kernel(FoldArgs<T> a) {
+    __shared__ double lds_v[4 * CH * kWave * kVec];  // one row per wave (gram path)
     const int s0 = a.batch_seg[a.batch], s1 = a.batch_seg[a.batch + 1];
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -136,6 +273,11 @@ __global__ __launch_bounds__(256) void transe_fold_kernel(FoldArgs<T> a) {
         RowReg<T, CH> V;
         V.load(ptr, a.n);
         bool dirty = false;
+        if (L1 && a.gram_min > 0 && p1 - p0 >= a.gram_min) {
+            fold_segment_gram<T, CH>(a, p0, p1, is_rel, V, lds_v + (threadIdx.x >> 6) * (CH * kWave * kVec), dirty);
+            if (dirty) V.store(ptr, a.n);
+            continue;
+        }
         for (int base = p0; base < p1; base += kWave) {
             // Prefetch up to 64 events: lane q holds event base+q.
             const int cnt = min(kWave, p1 - base);
