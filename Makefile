@@ -23,6 +23,12 @@ $(BINS): bin/kb2e
 kb2e_amd/libkb2e.so: $(CSRC)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ kb2e_amd/csrc/engine.hip
 
+# diagnostic build: per-phase cycle counters in the relation-owner kernels
+prof: kb2e_amd/libkb2e_prof.so
+
+kb2e_amd/libkb2e_prof.so: $(CSRC)
+	$(HIPCC) $(HIPFLAGS) -DKB2E_OWNER_PROF -shared -o $@ kb2e_amd/csrc/engine.hip
+
 oracle:
 	$(MAKE) -C oracle all
 
@@ -33,4 +39,4 @@ clean:
 	rm -f kb2e_amd/libkb2e.so bin/kb2e $(BINS)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle ref clean
+.PHONY: all oracle ref clean prof

@@ -142,7 +142,7 @@ struct kb2e_ctx {
     DevBuf aux, aux2;      // model-specific per-update exports
     // relation-owner schedule (TransH / TransR)
     RelOwnerPlan plan;
-    DevBuf owner, tickets, ent_done, wsnap, transr_work, owner_seg, dataflow_err, wtouched;
+    DevBuf owner, tickets, ent_done, wsnap, transr_work, owner_seg, dataflow_err, wtouched, desc, cdesc, ocount;
     int num_cus = 256;
     uint32_t batch_stamp = 0;
     int32_t gram_min = 48;  // KB2E_GRAM_MIN: fold segments this long use the scalar recurrence (0 = off)
@@ -990,6 +990,20 @@ kb2e_status kb2e_synchronize(kb2e_ctx* c) {
 kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
     return guarded(c, [&] {
         if (c->have_triples) reduce_stats(c, c->epoch_pos * c->B);
+#ifdef KB2E_OWNER_PROF
+        {
+            std::vector<unsigned long long> pr((size_t)kProfOwners * 16);
+            HIPCHK(hipMemcpyFromSymbol(pr.data(), HIP_SYMBOL(g_owner_prof), pr.size() * 8));
+            for (int o = 0; o < kProfOwners; ++o) {
+                if (!pr[(size_t)o * 16 + 11]) continue;
+                fprintf(stderr, "owner_prof %d", o);
+                for (int k = 0; k < 16; ++k) fprintf(stderr, " %llu", pr[(size_t)o * 16 + k]);
+                fprintf(stderr, "\n");
+            }
+            std::fill(pr.begin(), pr.end(), 0ull);
+            HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_owner_prof), pr.data(), pr.size() * 8));
+        }
+#endif
         if (loss) *loss = c->acc_loss;
         if (active) *active = c->acc_active;
         c->acc_loss = 0;

@@ -16,18 +16,25 @@ namespace kb2e {
 constexpr int kWave = 64;
 constexpr int kVec = 2;  // elements per lane per chunk
 
-// DPP row rotate (row_ror:N, N in 1..15) within each 16-lane row.
-template <int N>
-__device__ __forceinline__ float dpp_ror(float x) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x120 + N, 0xF, 0xF, false));
+// DPP lane moves.  Every lane the result is read from is written, so no
+// `old` operand (and no zero-initialisation) is needed.
+//   ROR<N>:  row_ror:N within each 16-lane row
+//   BC15:    row_bcast:15 (lane 15 of row k to every lane of row k+1)
+//   BC31:    row_bcast:31 (lane 31 to rows 2 and 3)
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
 }
-template <int N>
-__device__ __forceinline__ double dpp_ror(double x) {
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double x) {
     const long long b = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), 0x120 + N, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x120 + N, 0xF, 0xF, false);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffff), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
+template <int N, typename T>
+__device__ __forceinline__ T dpp_ror(T x) { return dpp_mov<0x120 + N>(x); }
+constexpr int kDppBcast15 = 0x142, kDppBcast31 = 0x143;
 
 __device__ __forceinline__ float readlane_f(float x, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
@@ -40,18 +47,32 @@ __device__ __forceinline__ double readlane_f(double x, int l) {
 }
 
 // Sum over the 64 lanes, identical in every lane.  Four DPP rotate steps make
-// every lane of a 16-lane row hold its row sum (each step pairs lanes
-// symmetrically, so all lanes of a row add the same two numbers); the four row
-// sums are then combined as (r0 + r1) + (r2 + r3) from scalar registers.  No
-// LDS traffic, ~5x shorter latency than a bpermute butterfly.
+// every lane of a 16-lane row k hold its row sum R_k (each step pairs lanes
+// symmetrically, so all lanes of a row add the same two numbers); two
+// row_bcast steps then leave (R3 + R2) + (R1 + R0) in row 3 (rows 0-2 end up
+// with partial or meaningless values), and lane 63 is broadcast.  The result
+// is bit-identical to (R0 + R1) + (R2 + R3).  No LDS traffic.
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
     v += dpp_ror<8>(v);
     v += dpp_ror<4>(v);
     v += dpp_ror<2>(v);
     v += dpp_ror<1>(v);
-    const T r0 = readlane_f(v, 0), r1 = readlane_f(v, 16), r2 = readlane_f(v, 32), r3 = readlane_f(v, 48);
-    return (r0 + r1) + (r2 + r3);
+    v += dpp_mov<kDppBcast15>(v);  // rows 1, 3: R1 + R0, R3 + R2
+    v += dpp_mov<kDppBcast31>(v);  // row 3: (R3 + R2) + (R1 + R0)
+    return readlane_f(v, 63);
+}
+
+// a / b for many a and one b, bit-identical to IEEE division: with y the
+// correctly rounded 1/b, q = RN(a y) is within an ulp of a/b, the residual
+// a - q b is exact by FMA, and RN(q + r y) is the correctly rounded quotient
+// (Markstein's theorem; no overflow / underflow in our ranges).  3 ops
+// instead of the ~10 of a full division.
+template <typename T>
+__device__ __forceinline__ T div_markstein(T a, T b, T y) {
+    const T q = a * y;
+    const T r = fma(-q, b, a);
+    return fma(r, y, q);
 }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }

@@ -354,6 +354,8 @@ struct OwnerArgs {
     const T* xreal;
     const T* scal;
     const T* snap;
+    const int32_t* batch_seg;
+    uint4* desc;         // TransR: per-position update descriptors of this batch
 };
 
 struct UpdateIds {
@@ -646,12 +648,44 @@ __global__ __launch_bounds__(256) void transr_compat_energy_kernel(RScoreArgs<T>
 
 // ---------------------------------------------------------- TransR phase B
 
+// Diagnostic build only (make prof): per-phase cycle accounting of the owner.
+#ifdef KB2E_OWNER_PROF
+constexpr int kProfOwners = 1024;
+__device__ unsigned long long g_owner_prof[kProfOwners][16];
+struct PhaseClock {
+    unsigned long long t, acc[16];
+    __device__ void start() {
+        for (int k = 0; k < 16; ++k) acc[k] = 0;
+        t = clock64();
+    }
+    __device__ void mark(int k) {
+        const unsigned long long n = clock64();
+        acc[k] += n - t;
+        t = n;
+    }
+    __device__ void count(int k) { acc[k] += 1; }
+    __device__ void flush() {
+        if (lane_id() == 0 && blockIdx.x < kProfOwners)
+            for (int k = 0; k < 16; ++k) atomicAdd(&g_owner_prof[blockIdx.x][k], acc[k]);
+    }
+};
+#define OWNER_PC_PARAM , PhaseClock& pc
+#define OWNER_PC_ARG , pc
+#define OWNER_MARK(k) pc.mark(k)
+#define OWNER_COUNT(k) pc.count(k)
+#else
+#define OWNER_PC_PARAM
+#define OWNER_PC_ARG
+#define OWNER_MARK(k)
+#define OWNER_COUNT(k)
+#endif
+
 // transRNorm (transr/trainer.cpp:35-64) on an entity row held in registers,
 // with the relation matrix W (n x ldl) in LDS and `abuf` (n) as broadcast
 // scratch.  Sums over j run in the reference's order for the check; the
 // per-column dot products of the iteration use the wave reduction.
 template <typename T, int CH>
-__device__ void transr_norm(RowReg<T, CH>& A, T* Wl, int ldl, T* abuf, int n, T lr) {
+__device__ void transr_norm(RowReg<T, CH>& A, T* Wl, int ldl, T* abuf, int n, T lr OWNER_PC_PARAM) {
     const int l = lane_id();
     for (int iter = 0; iter < 100000; ++iter) {
         A.store(abuf, n);
@@ -669,7 +703,9 @@ __device__ void transr_norm(RowReg<T, CH>& A, T* Wl, int ldl, T* abuf, int n, T 
             }
         xx = wave_sum(xx);
         __syncthreads();
+        OWNER_MARK(6);
         if (xx <= T(1)) break;
+        OWNER_COUNT(10);
         const T lambda = T(1);
         for (int i = 0; i < n; ++i) {
             T part = T(0);
@@ -695,6 +731,7 @@ __device__ void transr_norm(RowReg<T, CH>& A, T* Wl, int ldl, T* abuf, int n, T 
                 }
             __syncthreads();
         }
+        OWNER_MARK(7);
     }
 }
 
@@ -729,6 +766,10 @@ __global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32
     const int l = lane_id();
     const T lr = (T)a.lr;
     int cur = -1;
+#ifdef KB2E_OWNER_PROF
+    PhaseClock pc;
+    pc.start();
+#endif
     for (int p = p0; p < p1; ++p) {
         const uint64_t key = a.keys[p];
         const int kk = a.kl.kk_of(key);
@@ -744,7 +785,9 @@ __global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32
             cur = d.r;
             __syncthreads();
         }
+        OWNER_MARK(0);
         for (int q = 0; q < d.count; ++q) wait_ticket(a.done, d.ent[q], d.tick[q], a.err);
+        OWNER_MARK(1);
         // slots: head is slot 0; tail/entrel slots by identity
         int tslot = 0, eslot = 0;
         for (int q = 0; q < d.count; ++q) {
@@ -762,6 +805,7 @@ __global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32
             db[i] = dg[i];
         }
         __syncthreads();
+        OWNER_MARK(2);
         const T beta = d.u ? T(1) : T(-1);
         const T blr = beta * lr;
         // rank-1 update of W' (transr/trainer.cpp:167): W'[j][i] -= (blr x_i) d_j
@@ -769,6 +813,7 @@ __global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32
             const int j = idx / n, i = idx % n;
             Wl[j * ldl + i] = Wl[j * ldl + i] - (blr * xb[i]) * db[j];
         }
+        OWNER_MARK(3);
         // entity deltas with the snapshot matrix, summed over i in order (:168-169)
         const T* Ws = a.wsnap + (int64_t)d.r * n * a.ld;
         const bool same = tslot == 0;
@@ -803,6 +848,7 @@ __global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32
                 if (i < n) R.v[c][k] = R.v[c][k] - blr * xb[i];
             }
         __syncthreads();
+        OWNER_MARK(4);
         // unit norms (:174-180): r', h', t', then every row of W'
         R.norm(n, false);
         E[0].norm(n, false);
@@ -815,19 +861,394 @@ __global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32
         }
         __syncthreads();
         // transRNorm on head, tail and entity[relation] (:185-187)
-        transr_norm(E[0], Wl, ldl, abuf, n, lr);
-        transr_norm(E[tslot], Wl, ldl, abuf, n, lr);
-        transr_norm(E[eslot], Wl, ldl, abuf, n, lr);
+        OWNER_MARK(5);
+        transr_norm(E[0], Wl, ldl, abuf, n, lr OWNER_PC_ARG);
+        transr_norm(E[tslot], Wl, ldl, abuf, n, lr OWNER_PC_ARG);
+        transr_norm(E[eslot], Wl, ldl, abuf, n, lr OWNER_PC_ARG);
         R.store(a.rel + (int64_t)d.r * a.ld, n);
         for (int q = 0; q < d.count; ++q) row_store_sc1(E[q], a.ent + (int64_t)d.ent[q] * a.ld, n);
         drain_stores();
         for (int q = 0; q < d.count; ++q) release_ticket(a.done, d.ent[q], d.tick[q]);
+        OWNER_MARK(8);
+        OWNER_COUNT(11);
     }
     __syncthreads();
     if (cur >= 0) {
         w_spill(Wl, ldl, a.w + (int64_t)cur * n * a.ld, n, a.ld);
         if (l == 0) a.wtouched[cur] = stamp;
     }
+#ifdef KB2E_OWNER_PROF
+    pc.flush();
+#endif
+}
+
+// ------------------------------------------- TransR phase B, register owner
+//
+// For dim <= 64 (one element per lane).  Lane j keeps row j of the owner's
+// relation matrix W' in registers (w[]) and reads row j of the batch-start
+// snapshot from LDS (Ws, transposed so lane j's reads are consecutive), so the
+// rank-1 update, the deltas and the row norms are lane-local and fully
+// unrolled.  An LDS copy of W' (Wt, rows of ldl) is
+// refreshed only when transRNorm's check needs the column sums W'^T a.
+// Descriptors of every update (ids, slots, tickets) are precomputed in
+// parallel by transr_desc_kernel, so the serial owner loop does one uniform
+// load per update.
+
+// Descriptor of update (kk, u) at key position p: 3 x uint4
+//   q0 = {kk, u | count << 2 | roles0 << 4 | roles1 << 8 | roles2 << 12, r, 0}
+//   q1 = {ent0, ent1, ent2, 0}      q2 = {tick0, tick1, tick2, 0}
+// count == 0 marks an inactive update.
+template <typename T>
+__global__ __launch_bounds__(256) void transr_desc_kernel(OwnerArgs<T> a, int32_t ne) {
+    const int pb0 = a.seg_start[a.batch_seg[a.batch]];
+    const int pb1 = a.seg_start[a.batch_seg[a.batch + 1]];
+    for (int p = pb0 + blockIdx.x * blockDim.x + threadIdx.x; p < pb1; p += gridDim.x * blockDim.x) {
+        const uint64_t key = a.keys[p];
+        if (a.kl.row_of(key) < ne) continue;  // entity events
+        uint4* out = a.desc + (int64_t)(p - pb0) * 3;
+        const int kk = a.kl.kk_of(key);
+        if (!a.act[kk]) {
+            out[0] = make_uint4((uint32_t)kk, 0u, 0u, 0u);
+            continue;
+        }
+        const UpdateIds d = decode_update(a, key, true);
+        uint32_t packed = (uint32_t)d.u | ((uint32_t)d.count << 2);
+        for (int q = 0; q < d.count; ++q) packed |= d.roles[q] << (4 + 4 * q);
+        out[0] = make_uint4((uint32_t)kk, packed, (uint32_t)d.r, 0u);
+        out[1] = make_uint4((uint32_t)d.ent[0], d.count > 1 ? (uint32_t)d.ent[1] : 0u,
+                            d.count > 2 ? (uint32_t)d.ent[2] : 0u, 0u);
+        out[2] = make_uint4(d.tick[0], d.count > 1 ? d.tick[1] : 0u, d.count > 2 ? d.tick[2] : 0u, 0u);
+    }
+}
+
+// Per owner: the active descriptors of its segment, in order, packed to the
+// front of the segment's slice (cdesc[(p0 - pb0) + i]), and their count.
+__global__ __launch_bounds__(256) void transr_compact_kernel(const int32_t* owner_seg, const int32_t* seg_start,
+                                                             const int32_t* batch_seg, int32_t batch, int32_t owners,
+                                                             const uint4* desc, uint4* cdesc, int32_t* ocount) {
+    __shared__ int wave_tot[4];
+    const int o = blockIdx.x;
+    const int seg = owner_seg[(int64_t)batch * owners + o];
+    if (seg < 0) {
+        if (threadIdx.x == 0) ocount[o] = 0;
+        return;
+    }
+    const int p0 = seg_start[seg], p1 = seg_start[seg + 1];
+    const int pb0 = seg_start[batch_seg[batch]];
+    const int base = p0 - pb0;
+    const int wv = threadIdx.x >> 6, l = lane_id();
+    int running = 0;
+    for (int chunk = p0; chunk < p1; chunk += 256) {
+        const int p = chunk + threadIdx.x;
+        uint4 q0{}, q1{}, q2{};
+        bool active = false;
+        if (p < p1) {
+            const uint4* d = desc + (int64_t)(p - pb0) * 3;
+            q0 = d[0];
+            active = ((q0.y >> 2) & 3u) != 0;
+            if (active) {
+                q1 = d[1];
+                q2 = d[2];
+            }
+        }
+        const uint64_t m = __ballot(active);
+        if (l == 0) wave_tot[wv] = __popcll(m);
+        __syncthreads();
+        int before = __popcll(m & ((1ull << l) - 1ull));
+        for (int k = 0; k < wv; ++k) before += wave_tot[k];
+        const int total = wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
+        if (active) {
+            uint4* out = cdesc + (int64_t)(base + running + before) * 3;
+            out[0] = q0;
+            out[1] = q1;
+            out[2] = q2;
+        }
+        running += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) ocount[o] = running;
+}
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// Wait until done[e_q] == tick_q for every slot (polls issued together).
+__device__ __forceinline__ void wait_tickets3(const uint32_t* done, int count, const uint32_t* e, const uint32_t* tk,
+                                              uint32_t* err) {
+    uint32_t spins = 0;
+    for (;;) {
+        const uint32_t f0 = __hip_atomic_load((gu32*)(done + e[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t f1 = count > 1 ? __hip_atomic_load((gu32*)(done + e[1]), __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT) : tk[1];
+        const uint32_t f2 = count > 2 ? __hip_atomic_load((gu32*)(done + e[2]), __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT) : tk[2];
+        if (f0 == tk[0] && f1 == tk[1] && f2 == tk[2]) return;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 26)) {
+            __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+}
+
+// LDS row stride of the W' copy: = 1 (mod 16) doubles, so lane j writing row
+// j and lane i reading column i are both (nearly) conflict-free.
+__host__ __device__ constexpr int transr_ldl(int nm) { return ((nm + 14) / 16) * 16 + 1; }
+
+template <typename T, int NM>
+__host__ __device__ constexpr size_t transr_reg_lds_bytes() {
+    return ((size_t)NM * transr_ldl(NM) + kWave + 2 * kWave + (size_t)NM * kWave) * sizeof(T);
+}
+
+// transRNorm (transr/trainer.cpp:35-64) on the entity element `al` of this
+// lane, W' rows in registers.  Every loop runs over the NM register slots
+// without per-element guards: slots >= n (and lanes >= n) hold exact zeros,
+// so their terms add +0 and leave the sums unchanged.  The check's column
+// sums (four interleaved partial sums over j, from the LDS copy) decide the
+// loop and seed column 0 of an iteration; later columns use the wave
+// reduction.  Every element update is the reference's operation.
+template <typename T, int NM>
+__device__ __forceinline__ T transr_norm_reg(T al, T (&w)[NM], T* Wt, T* abuf, int n, T lr2, bool& dirty
+                                             OWNER_PC_PARAM) {
+    constexpr int ldl = transr_ldl(NM);
+    const int l = lane_id();
+    for (int iter = 0; iter < 100000; ++iter) {
+        if (dirty) {
+            if (l < NM) {
+#pragma unroll
+                for (int i = 0; i < NM; ++i) Wt[l * ldl + i] = w[i];
+            }
+            dirty = false;
+        }
+        abuf[l] = al;
+        wave_lds_sync();
+        // four interleaved partial sums (the value only decides x <= 1 and
+        // seeds column 0, like the reduced sums of the later columns).  The
+        // LDS reads are staged in double-buffered chunks so a chunk's reads
+        // are in flight while the previous chunk is multiplied.
+        constexpr int CK = 10;
+        constexpr int NCK = (NM + CK - 1) / CK;
+        T y4[4] = {T(0), T(0), T(0), T(0)};
+        T wc[2][CK], ab[2][CK];
+#pragma unroll
+        for (int q = 0; q < CK; ++q) {
+            wc[0][q] = q < NM ? Wt[q * ldl + l] : T(0);
+            ab[0][q] = q < NM ? abuf[q] : T(0);
+        }
+#pragma unroll
+        for (int c = 0; c < NCK; ++c) {
+            if (c + 1 < NCK) {
+#pragma unroll
+                for (int q = 0; q < CK; ++q) {
+                    const int j = (c + 1) * CK + q;
+                    wc[(c + 1) & 1][q] = j < NM ? Wt[j * ldl + l] : T(0);
+                    ab[(c + 1) & 1][q] = j < NM ? abuf[j] : T(0);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < CK; ++q) {
+                const int j = c * CK + q;
+                if (j < NM) y4[j & 3] += wc[c & 1][q] * ab[c & 1][q];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const T y = (y4[0] + y4[1]) + (y4[2] + y4[3]);
+        const T xx = wave_sum(l < n ? y * y : T(0));
+        OWNER_MARK(6);
+        if (xx <= T(1)) break;
+        OWNER_COUNT(10);
+        const T tmp0 = readlane_f(y, 0);
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+            const T tmp = i == 0 ? tmp0 : wave_sum(w[i] * al);
+            // learningRate_ * lambda * (2 tmp), lambda = 1: the doubling is exact,
+            // so (2 lr) * tmp rounds the same real number once, as the reference
+            const T coef = lr2 * tmp;
+            w[i] = w[i] - coef * al;
+            al = al - coef * w[i];
+        }
+        dirty = true;
+        OWNER_MARK(7);
+    }
+    return al;
+}
+
+// NM >= n register slots per lane (NM == n for the instantiated common dims).
+template <typename T, int NM>
+__global__ __launch_bounds__(64) void transr_owner_reg_kernel(OwnerArgs<T> a, const uint4* cdesc, const int32_t* ocount,
+                                                              uint32_t stamp) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int ldl = transr_ldl(NM);
+    const int seg = a.owner_seg[(int64_t)a.batch * a.owners + blockIdx.x];
+    if (seg < 0) return;
+    const int m = ocount[blockIdx.x];
+    const uint4* dl0 = cdesc + (int64_t)(a.seg_start[seg] - a.seg_start[a.batch_seg[a.batch]]) * 3;
+    const int n = a.n, ld = a.ld;
+    T* Wt = (T*)smem;               // NM rows of ldl (+ slack: lanes >= NM read past the last row)
+    T* abuf = Wt + NM * ldl + kWave;  // [64] transRNorm broadcast
+    T* xs = abuf + kWave;           // [64] beta * lr * x_i, zero past n
+    T* Ws = xs + kWave;             // [NM][64]: Ws[i * 64 + j] = snapshot W[j][i], zero past n
+    const int l = lane_id();
+    const bool row_lane = l < n;
+    const T lr = (T)a.lr;
+    const T lr2 = T(2) * lr;        // lr * (2 tmp) == (2 lr) * tmp exactly
+    T w[NM];
+#pragma unroll
+    for (int i = 0; i < NM; ++i) w[i] = T(0);
+    int cur = -1;
+    T rl = T(0);
+    bool dirty = true;
+#ifdef KB2E_OWNER_PROF
+    PhaseClock pc;
+    pc.start();
+#endif
+    // software pipeline: descriptor of update it+1 and its x / d elements are
+    // loaded during update it.
+    uint4 n0{}, n1{}, n2{};
+    T nxl = T(0), ndl = T(0);
+    if (m > 0) {
+        n0 = dl0[0];
+        n1 = dl0[1];
+        n2 = dl0[2];
+        const int64_t xo = ((int64_t)uni(n0.x) * 2 + (uni(n0.y) & 1)) * ld;
+        nxl = row_lane ? a.xreal[xo + l] : T(0);
+        ndl = row_lane ? a.scal[xo + l] : T(0);
+    }
+    for (int it = 0; it < m; ++it) {
+        const uint4 q0 = n0, q1 = n1, q2 = n2;
+        const T xl = nxl, dl = ndl;
+        if (it + 1 < m) {
+            const uint4* dn = dl0 + (int64_t)(it + 1) * 3;
+            n0 = dn[0];
+            n1 = dn[1];
+            n2 = dn[2];
+        }
+        const uint32_t packed = uni(q0.y);
+        const int count = (int)((packed >> 2) & 3);
+        const int kk = (int)uni(q0.x), u = (int)(packed & 1), r = (int)uni(q0.z);
+        (void)kk;
+        const uint32_t ent[3] = {uni(q1.x), uni(q1.y), uni(q1.z)};
+        const uint32_t tk[3] = {uni(q2.x), uni(q2.y), uni(q2.z)};
+        const int ts = ((packed >> 8) & kRoleTail) ? 1 : 0;  // tail is slot 0 or 1
+        const int es = ((packed >> 4) & kRoleEntRel) ? 0 : (((packed >> 8) & kRoleEntRel) ? 1 : 2);
+        (void)count;
+        if (r != cur) {
+            if (cur >= 0 && row_lane) {
+                T* dst = a.w + ((int64_t)cur * n + l) * ld;
+#pragma unroll
+                for (int i = 0; i < NM; ++i)
+                    if (i < n) dst[i] = w[i];
+            }
+            if (cur >= 0 && l == 0) a.wtouched[cur] = stamp;
+            drain_stores();  // a relation met again re-reads what this wave stored
+            const T* src = a.w + ((int64_t)r * n + l) * ld;
+            const T* srs = a.wsnap + ((int64_t)r * n + l) * ld;
+#pragma unroll
+            for (int i = 0; i < NM; ++i) {
+                w[i] = (row_lane && i < n) ? load_sc1(src + i) : T(0);
+                Ws[i * kWave + l] = (row_lane && i < n) ? srs[i] : T(0);
+            }
+            rl = row_lane ? load_sc1(a.rel + (int64_t)r * ld + l) : T(0);
+            cur = r;
+        }
+        if (it + 1 < m) {  // x / d of the next update
+            const int64_t xo = ((int64_t)uni(n0.x) * 2 + (uni(n0.y) & 1)) * ld;
+            nxl = row_lane ? a.xreal[xo + l] : T(0);
+            ndl = row_lane ? a.scal[xo + l] : T(0);
+        }
+        OWNER_MARK(0);
+        // ---- relation state: transr/trainer.cpp:147-171 (W', r') and :174-180 (norms)
+        const T blr = (u ? T(1) : T(-1)) * lr;  // beta * learningRate_
+        xs[l] = blr * xl;  // dl: snapshot head - tail, element l
+        wave_lds_sync();
+        // W'[j][i] -= (blr x_i) d_j ; lane j owns row j
+#pragma unroll
+        for (int i = 0; i < NM; ++i) w[i] = w[i] - xs[i] * dl;
+        rl = rl - xs[l];
+        {
+            const T len = sqrt(wave_sum(rl * rl));
+            if (row_lane) rl = rl / len;
+        }
+        if (row_lane) {
+            T sq = T(0);
+#pragma unroll
+            for (int i = 0; i < NM; ++i) sq += w[i] * w[i];
+            const T len = sqrt(sq);
+            const T inv = T(1) / len;
+#pragma unroll
+            for (int i = 0; i < NM; ++i) w[i] = div_markstein(w[i], len, inv);
+            a.rel[(int64_t)r * ld + l] = rl;
+        }
+        dirty = true;
+        OWNER_MARK(3);
+        // ---- entity rows
+        wait_tickets3(a.done, count, ent, tk, a.err);
+        OWNER_MARK(1);
+        T v0 = row_lane ? load_sc1(a.ent + (int64_t)ent[0] * ld + l) : T(0);
+        T v1 = (count > 1 && row_lane) ? load_sc1(a.ent + (int64_t)ent[1] * ld + l) : T(0);
+        T v2 = (count > 2 && row_lane) ? load_sc1(a.ent + (int64_t)ent[2] * ld + l) : T(0);
+        OWNER_MARK(2);
+        // deltas with the snapshot matrix, subtracted in order of i (:168-169)
+        if (ts == 0) {
+#pragma unroll
+            for (int i = 0; i < NM; ++i) {
+                const T g = xs[i] * Ws[i * kWave + l];
+                v0 = v0 - g;
+                v0 = v0 + g;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NM; ++i) {
+                const T g = xs[i] * Ws[i * kWave + l];
+                v0 = v0 - g;
+                v1 = v1 + g;
+            }
+        }
+        // common::norm(head), common::norm(tail) (:175-176)
+        {
+            const T len = sqrt(wave_sum(v0 * v0));
+            if (row_lane) v0 = v0 / len;
+        }
+        {
+            T tv = ts == 0 ? v0 : v1;
+            const T len = sqrt(wave_sum(tv * tv));
+            if (row_lane) tv = tv / len;
+            if (ts == 0) v0 = tv;
+            else v1 = tv;
+        }
+        OWNER_MARK(4);
+        // transRNorm on head, tail, entity[relation] (:185-187); a slot is
+        // published as soon as no later call touches it.
+#pragma unroll 1
+        for (int call = 0; call < 3; ++call) {
+            const int s = call == 0 ? 0 : (call == 1 ? ts : es);
+            T al = s == 0 ? v0 : (s == 1 ? v1 : v2);
+            al = transr_norm_reg<T, NM>(al, w, Wt, abuf, n, lr2, dirty OWNER_PC_ARG);
+            if (s == 0) v0 = al;
+            else if (s == 1) v1 = al;
+            else v2 = al;
+            const bool later = (call == 0 && (ts == s || es == s)) || (call == 1 && es == s);
+            if (!later) {
+                if (row_lane) store_sc1(a.ent + (int64_t)ent[s] * ld + l, al);
+                drain_stores();
+                release_ticket(a.done, (int)ent[s], tk[s]);
+            }
+        }
+        OWNER_MARK(8);
+        OWNER_COUNT(11);
+    }
+    if (cur >= 0) {
+        if (row_lane) {
+            T* dst = a.w + ((int64_t)cur * n + l) * ld;
+#pragma unroll
+            for (int i = 0; i < NM; ++i)
+                if (i < n) dst[i] = w[i];
+        }
+        if (l == 0) a.wtouched[cur] = stamp;
+    }
+#ifdef KB2E_OWNER_PROF
+    pc.flush();
+#endif
 }
 
 // After phase B: the committed matrices (snapshot table) take the new values

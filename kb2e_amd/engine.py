@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libkb2e.so")
+LIB_PATH = os.environ.get("KB2E_LIB") or os.path.join(HERE, "libkb2e.so")
 
 MODELS = {"transe": 0, "transh": 1, "transr": 2, "E": 0, "H": 1, "R": 2}
 STATUS = {0: "OK", 1: "EINVAL", 2: "EDEVICE", 3: "ESTATE", 4: "ENOMEM", 5: "EUNSUPPORTED", 6: "ESAMPLER"}
