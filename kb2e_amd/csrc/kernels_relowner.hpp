@@ -324,6 +324,38 @@ __device__ __forceinline__ void orth_norm(RowReg<T, CH>& A, RowReg<T, CH>& Bv, i
     Bv.norm(n, false);
 }
 
+// Diagnostic build only (make prof): per-phase cycle accounting of the owner.
+#ifdef KB2E_OWNER_PROF
+constexpr int kProfOwners = 1024;
+__device__ unsigned long long g_owner_prof[kProfOwners][16];
+struct PhaseClock {
+    unsigned long long t, acc[16];
+    __device__ void start() {
+        for (int k = 0; k < 16; ++k) acc[k] = 0;
+        t = clock64();
+    }
+    __device__ void mark(int k) {
+        const unsigned long long n = clock64();
+        acc[k] += n - t;
+        t = n;
+    }
+    __device__ void count(int k) { acc[k] += 1; }
+    __device__ void flush() {
+        if (lane_id() == 0 && blockIdx.x < kProfOwners)
+            for (int k = 0; k < 16; ++k) atomicAdd(&g_owner_prof[blockIdx.x][k], acc[k]);
+    }
+};
+#define OWNER_PC_PARAM , PhaseClock& pc
+#define OWNER_PC_ARG , pc
+#define OWNER_MARK(k) pc.mark(k)
+#define OWNER_COUNT(k) pc.count(k)
+#else
+#define OWNER_PC_PARAM
+#define OWNER_PC_ARG
+#define OWNER_MARK(k)
+#define OWNER_COUNT(k)
+#endif
+
 // ---------------------------------------------------------- TransH phase B
 
 template <typename T>
@@ -400,79 +432,339 @@ __device__ __forceinline__ UpdateIds decode_update(const OwnerArgs<T>& a, uint64
     return d;
 }
 
-template <typename T, int CH>
-__global__ __launch_bounds__(64) void transh_owner_kernel(OwnerArgs<T> a) {
-    const int seg = a.owner_seg[(int64_t)a.batch * a.owners + blockIdx.x];
-    if (seg < 0) return;
-    const int p0 = a.seg_start[seg], p1 = a.seg_start[seg + 1];
-    const int n = a.n;
-    const T lr = (T)a.lr;
-    for (int p = p0; p < p1; ++p) {
+// Descriptor of update (kk, u) at key position p: 3 x uint4
+//   q0 = {kk, u | count << 2 | roles0 << 4 | roles1 << 8 | roles2 << 12, r, 0}
+//   q1 = {ent0, ent1, ent2, 0}      q2 = {tick0, tick1, tick2, 0}
+// count == 0 marks an inactive update.
+template <typename T>
+__global__ __launch_bounds__(256) void relowner_desc_kernel(OwnerArgs<T> a, int32_t ne, int32_t entrel) {
+    const int pb0 = a.seg_start[a.batch_seg[a.batch]];
+    const int pb1 = a.seg_start[a.batch_seg[a.batch + 1]];
+    for (int p = pb0 + blockIdx.x * blockDim.x + threadIdx.x; p < pb1; p += gridDim.x * blockDim.x) {
         const uint64_t key = a.keys[p];
+        if (a.kl.row_of(key) < ne) continue;  // entity events
+        uint4* out = a.desc + (int64_t)(p - pb0) * 3;
         const int kk = a.kl.kk_of(key);
-        if (!a.act[kk]) continue;
-        const UpdateIds d = decode_update(a, key, false);
-        for (int q = 0; q < d.count; ++q) wait_ticket(a.done, d.ent[q], d.tick[q], a.err);
-        RowReg<T, CH> E0, E1, R, W;
-        row_load_sc1(E0, a.ent + (int64_t)d.ent[0] * a.ld, n);
-        if (d.count > 1) row_load_sc1(E1, a.ent + (int64_t)d.ent[1] * a.ld, n);
-        R.load(a.rel + (int64_t)d.r * a.ld, n);
-        W.load(a.w + (int64_t)d.r * a.ld, n);
-        // head row = E0; tail row = E0 (h == t) or E1
-        const bool same = d.count == 1;
-        const T* sc = a.scal + ((int64_t)kk * 2 + d.u) * 4;
-        const T hs = sc[0], ts = sc[1], sumx = sc[2];
-        const uint64_t* xw = a.xbits + ((int64_t)kk * 2 + d.u) * a.nw;
-        uint64_t words[2 * CH];
+        if (!a.act[kk]) {
+            out[0] = make_uint4((uint32_t)kk, 0u, 0u, 0u);
+            continue;
+        }
+        const UpdateIds d = decode_update(a, key, entrel != 0);
+        uint32_t packed = (uint32_t)d.u | ((uint32_t)d.count << 2);
+        for (int q = 0; q < d.count; ++q) packed |= d.roles[q] << (4 + 4 * q);
+        out[0] = make_uint4((uint32_t)kk, packed, (uint32_t)d.r, 0u);
+        out[1] = make_uint4((uint32_t)d.ent[0], d.count > 1 ? (uint32_t)d.ent[1] : 0u,
+                            d.count > 2 ? (uint32_t)d.ent[2] : 0u, 0u);
+        out[2] = make_uint4(d.tick[0], d.count > 1 ? d.tick[1] : 0u, d.count > 2 ? d.tick[2] : 0u, 0u);
+    }
+}
+
+// Per owner: the active descriptors of its segment, in order, packed to the
+// front of the segment's slice (cdesc[(p0 - pb0) + i]), and their count.
+__global__ __launch_bounds__(256) void relowner_compact_kernel(const int32_t* owner_seg, const int32_t* seg_start,
+                                                             const int32_t* batch_seg, int32_t batch, int32_t owners,
+                                                             const uint4* desc, uint4* cdesc, int32_t* ocount) {
+    __shared__ int wave_tot[4];
+    const int o = blockIdx.x;
+    const int seg = owner_seg[(int64_t)batch * owners + o];
+    if (seg < 0) {
+        if (threadIdx.x == 0) ocount[o] = 0;
+        return;
+    }
+    const int p0 = seg_start[seg], p1 = seg_start[seg + 1];
+    const int pb0 = seg_start[batch_seg[batch]];
+    const int base = p0 - pb0;
+    const int wv = threadIdx.x >> 6, l = lane_id();
+    int running = 0;
+    for (int chunk = p0; chunk < p1; chunk += 256) {
+        const int p = chunk + threadIdx.x;
+        uint4 q0{}, q1{}, q2{};
+        bool active = false;
+        if (p < p1) {
+            const uint4* d = desc + (int64_t)(p - pb0) * 3;
+            q0 = d[0];
+            active = ((q0.y >> 2) & 3u) != 0;
+            if (active) {
+                q1 = d[1];
+                q2 = d[2];
+            }
+        }
+        const uint64_t m = __ballot(active);
+        if (l == 0) wave_tot[wv] = __popcll(m);
+        __syncthreads();
+        int before = __popcll(m & ((1ull << l) - 1ull));
+        for (int k = 0; k < wv; ++k) before += wave_tot[k];
+        const int total = wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
+        if (active) {
+            uint4* out = cdesc + (int64_t)(base + running + before) * 3;
+            out[0] = q0;
+            out[1] = q1;
+            out[2] = q2;
+        }
+        running += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) ocount[o] = running;
+}
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// Wait until done[e_q] == tick_q for every slot (polls issued together).
+__device__ __forceinline__ void wait_tickets3(const uint32_t* done, int count, const uint32_t* e, const uint32_t* tk,
+                                              uint32_t* err) {
+    uint32_t spins = 0;
+    for (;;) {
+        const uint32_t f0 = __hip_atomic_load((gu32*)(done + e[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t f1 = count > 1 ? __hip_atomic_load((gu32*)(done + e[1]), __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT) : tk[1];
+        const uint32_t f2 = count > 2 ? __hip_atomic_load((gu32*)(done + e[2]), __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT) : tk[2];
+        if (f0 == tk[0] && f1 == tk[1] && f2 == tk[2]) return;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 26)) {
+            __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+}
+
+// common::norm on independent rows at once (the reductions overlap): the
+// first rows with ignoreShort = true, the last one (w) with false.
+template <typename T, int CH>
+__device__ __forceinline__ void scale_row(RowReg<T, CH>& A, T len, bool apply, int n) {
+    if (!apply) return;
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int k = 0; k < kVec; ++k)
+            if (elem_valid(c, k, n)) A.v[c][k] = A.v[c][k] / len;
+}
+template <typename T, int CH>
+__device__ __forceinline__ void norm_rows3(RowReg<T, CH>& A, RowReg<T, CH>& B, RowReg<T, CH>& Wn, int n) {
+    T sa = T(0), sb = T(0), sw = T(0);
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            sa += A.v[c][k] * A.v[c][k];
+            sb += B.v[c][k] * B.v[c][k];
+            sw += Wn.v[c][k] * Wn.v[c][k];
+        }
+    const T la = sqrt(wave_sum(sa)), lb = sqrt(wave_sum(sb)), lw = sqrt(wave_sum(sw));
+    scale_row(A, la, la > T(1), n);
+    scale_row(B, lb, lb > T(1), n);
+    scale_row(Wn, lw, true, n);
+}
+template <typename T, int CH>
+__device__ __forceinline__ void norm_rows4(RowReg<T, CH>& A, RowReg<T, CH>& B, RowReg<T, CH>& C,
+                                           RowReg<T, CH>& Wn, int n) {
+    T sa = T(0), sb = T(0), sc = T(0), sw = T(0);
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            sa += A.v[c][k] * A.v[c][k];
+            sb += B.v[c][k] * B.v[c][k];
+            sc += C.v[c][k] * C.v[c][k];
+            sw += Wn.v[c][k] * Wn.v[c][k];
+        }
+    const T la = sqrt(wave_sum(sa)), lb = sqrt(wave_sum(sb)), lc = sqrt(wave_sum(sc)), lw = sqrt(wave_sum(sw));
+    scale_row(A, la, la > T(1), n);
+    scale_row(B, lb, lb > T(1), n);
+    scale_row(C, lc, lc > T(1), n);
+    scale_row(Wn, lw, true, n);
+}
+
+// Per-update inputs of a TransH update exported by phase A.
+template <typename T, int CH>
+struct HUpdateIn {
+    RowReg<T, CH> SH, ST;  // snapshot head / tail rows
+    uint64_t words[2 * CH];
+    T hs, ts, sumx;
+    __device__ __forceinline__ void load(const OwnerArgs<T>& a, uint4 q0, int n) {
+        const int kk = (int)uni(q0.x), u = (int)(uni(q0.y) & 1);
+        const int64_t ku = (int64_t)kk * 2 + u;
+        SH.load(a.snap + (ku * 2 + 0) * a.ld, n);
+        ST.load(a.snap + (ku * 2 + 1) * a.ld, n);
+        const uint64_t* xw = a.xbits + ku * a.nw;
 #pragma unroll
         for (int q = 0; q < 2 * CH; ++q) words[q] = xw[q];
-        const T beta = d.u ? T(1) : T(-1);
+        const T* sc = a.scal + ku * 4;
+        hs = sc[0];
+        ts = sc[1];
+        sumx = sc[2];
+    }
+};
+
+// One persistent workgroup per owner walks its compacted update list; the
+// relation state (r, w) stays in registers while consecutive updates share the
+// relation, and the next update's descriptor and phase-A inputs are loaded
+// during the current one.  Entity rows move through tickets as documented at
+// the top of this file.
+template <typename T, int CH>
+__global__ __launch_bounds__(64) void transh_owner_kernel(OwnerArgs<T> a, const uint4* cdesc, const int32_t* ocount) {
+    const int seg = a.owner_seg[(int64_t)a.batch * a.owners + blockIdx.x];
+    if (seg < 0) return;
+    const int m = ocount[blockIdx.x];
+    const uint4* dl0 = cdesc + (int64_t)(a.seg_start[seg] - a.seg_start[a.batch_seg[a.batch]]) * 3;
+    const int n = a.n;
+    const T lr = (T)a.lr;
+#ifdef KB2E_OWNER_PROF
+    PhaseClock pc;
+    pc.start();
+#endif
+    RowReg<T, CH> R, W;
+    int cur = -1;
+    // pipeline: descriptors run two updates ahead, phase-A inputs one ahead
+    uint4 n0{}, n1{}, n2{}, f0{}, f1{}, f2{};
+    HUpdateIn<T, CH> nin;
+    if (m > 0) {
+        n0 = dl0[0];
+        n1 = dl0[1];
+        n2 = dl0[2];
+        nin.load(a, n0, n);
+    }
+    if (m > 1) {
+        f0 = dl0[3];
+        f1 = dl0[4];
+        f2 = dl0[5];
+    }
+    for (int it = 0; it < m; ++it) {
+        const uint4 q0 = n0, q1 = n1, q2 = n2;
+        const HUpdateIn<T, CH> in = nin;
+        n0 = f0;
+        n1 = f1;
+        n2 = f2;
+        if (it + 2 < m) {
+            const uint4* dn = dl0 + (int64_t)(it + 2) * 3;
+            f0 = dn[0];
+            f1 = dn[1];
+            f2 = dn[2];
+        }
+        const uint32_t packed = uni(q0.y);
+        const int count = (int)((packed >> 2) & 3);
+        const int u = (int)(packed & 1), r = (int)uni(q0.z);
+        const uint32_t ent[3] = {uni(q1.x), uni(q1.y), 0u};
+        const uint32_t tk[3] = {uni(q2.x), uni(q2.y), 0u};
+        if (r != cur) {
+            if (cur >= 0) {
+                R.store(a.rel + (int64_t)cur * a.ld, n);
+                W.store(a.w + (int64_t)cur * a.ld, n);
+            }
+            drain_stores();  // a relation met again re-reads what this wave stored
+            row_load_sc1(R, a.rel + (int64_t)r * a.ld, n);
+            row_load_sc1(W, a.w + (int64_t)r * a.ld, n);
+            cur = r;
+        }
+        if (it + 1 < m) nin.load(a, n0, n);
+        OWNER_MARK(0);
+        wait_tickets3(a.done, count, ent, tk, a.err);
+        OWNER_MARK(1);
+        RowReg<T, CH> E0, E1;
+        row_load_sc1(E0, a.ent + (int64_t)ent[0] * a.ld, n);
+        if (count > 1) row_load_sc1(E1, a.ent + (int64_t)ent[1] * a.ld, n);
+        else E1.load(nullptr, 0);  // zeros
+        // head row = E0; tail row = E0 (h == t) or E1
+        const bool same = count == 1;
+        const T beta = u ? T(1) : T(-1);
         const T blr = beta * lr;  // beta * learningRate_
-        RowReg<T, CH> SH, ST;     // snapshot head / tail rows
-        SH.load(a.snap + (((int64_t)kk * 2 + d.u) * 2 + 0) * a.ld, n);
-        ST.load(a.snap + (((int64_t)kk * 2 + d.u) * 2 + 1) * a.ld, n);
+        OWNER_MARK(2);
         // transh/trainer.cpp:23-41
 #pragma unroll
         for (int c = 0; c < CH; ++c)
 #pragma unroll
             for (int k = 0; k < kVec; ++k) {
                 if (!elem_valid(c, k, n)) continue;
-                const T x = xbit(words, c, k) ? T(1) : T(-1);
+                const T x = xbit(in.words, c, k) ? T(1) : T(-1);
                 const T dlt = blr * x;
                 R.v[c][k] = R.v[c][k] - dlt;
                 E0.v[c][k] = E0.v[c][k] - dlt;
                 if (same) E0.v[c][k] = E0.v[c][k] + dlt;
                 else E1.v[c][k] = E1.v[c][k] + dlt;
-                W.v[c][k] = W.v[c][k] + dlt * hs;
-                W.v[c][k] = W.v[c][k] - dlt * ts;
+                W.v[c][k] = W.v[c][k] + dlt * in.hs;
+                W.v[c][k] = W.v[c][k] - dlt * in.ts;
             }
         // transh/trainer.cpp:43-46
-        const T g = blr * sumx;
+        const T g = blr * in.sumx;
 #pragma unroll
         for (int c = 0; c < CH; ++c)
 #pragma unroll
             for (int k = 0; k < kVec; ++k) {
                 if (!elem_valid(c, k, n)) continue;
-                W.v[c][k] = W.v[c][k] + g * SH.v[c][k];
-                W.v[c][k] = W.v[c][k] - g * ST.v[c][k];
+                W.v[c][k] = W.v[c][k] + g * in.SH.v[c][k];
+                W.v[c][k] = W.v[c][k] - g * in.ST.v[c][k];
             }
-        // transh/trainer.cpp:48-58
-        R.norm(n, true);
-        E0.norm(n, true);
-        if (same) E0.norm(n, true);
-        else E1.norm(n, true);
-        W.norm(n, false);
-        orth_norm(R, W, n, lr);
-        orth_norm(E0, W, n, lr);
-        if (same) orth_norm(E0, W, n, lr);
-        else orth_norm(E1, W, n, lr);
-        R.store(a.rel + (int64_t)d.r * a.ld, n);
-        W.store(a.w + (int64_t)d.r * a.ld, n);
-        row_store_sc1(E0, a.ent + (int64_t)d.ent[0] * a.ld, n);
-        if (!same) row_store_sc1(E1, a.ent + (int64_t)d.ent[1] * a.ld, n);
+        OWNER_MARK(3);
+        // transh/trainer.cpp:48-58: norm(r), norm(h), norm(t), norm(w, false),
+        // then normOrth (common/utils.cpp:79-111) of r, h, t against w.
+        // normOrth only moves a row when x = w.row > 0.1, which is rare; all
+        // norms and the three x come from one round of raw sums, so the common
+        // case costs one (7-way interleaved) reduction round.  There r', h', t'
+        // get exactly the reference's single division by their length, and w'
+        // is divided by its length once: the reference's further divisions of
+        // w' by its (already unit) length inside normOrth are 1 +- ulp and are
+        // the only difference.  Any x > 0.1 replays the reference's sequence
+        // step by step on the untouched rows.
+        T sR = T(0), s0 = T(0), s1 = T(0), sW = T(0), dR = T(0), d0 = T(0), d1 = T(0);
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) {
+                sR += R.v[c][k] * R.v[c][k];
+                s0 += E0.v[c][k] * E0.v[c][k];
+                s1 += E1.v[c][k] * E1.v[c][k];
+                sW += W.v[c][k] * W.v[c][k];
+                dR += W.v[c][k] * R.v[c][k];
+                d0 += W.v[c][k] * E0.v[c][k];
+                d1 += W.v[c][k] * E1.v[c][k];
+            }
+        sR = wave_sum(sR);
+        s0 = wave_sum(s0);
+        s1 = wave_sum(s1);
+        sW = wave_sum(sW);
+        dR = wave_sum(dR);
+        d0 = wave_sum(d0);
+        d1 = wave_sum(d1);
+        const T lR = sqrt(sR), l0 = sqrt(s0), l1 = sqrt(s1), lW = sqrt(sW);
+        const T cR = lR > T(1) ? lR : T(1), c0 = l0 > T(1) ? l0 : T(1), c1 = l1 > T(1) ? l1 : T(1);
+        const bool fast = dR / (lW * cR) <= T(0.1) && d0 / (lW * c0) <= T(0.1) &&
+                          (same || d1 / (lW * c1) <= T(0.1));
+        OWNER_MARK(4);
+        if (fast) {
+            scale_row(R, lR, lR > T(1), n);
+            scale_row(E0, l0, l0 > T(1), n);
+            if (same) E0.norm(n, true);
+            else scale_row(E1, l1, l1 > T(1), n);
+            scale_row(W, lW, true, n);
+            OWNER_MARK(6);
+        } else {
+            if (same) {
+                norm_rows3(R, E0, W, n);
+                E0.norm(n, true);
+            } else {
+                norm_rows4(R, E0, E1, W, n);
+            }
+            orth_norm(R, W, n, lr);
+            orth_norm(E0, W, n, lr);
+            if (same) orth_norm(E0, W, n, lr);
+            else orth_norm(E1, W, n, lr);
+            OWNER_MARK(7);
+        }
+        row_store_sc1(E0, a.ent + (int64_t)ent[0] * a.ld, n);
+        if (!same) row_store_sc1(E1, a.ent + (int64_t)ent[1] * a.ld, n);
         drain_stores();
-        for (int q = 0; q < d.count; ++q) release_ticket(a.done, d.ent[q], d.tick[q]);
+        release_ticket(a.done, (int)ent[0], tk[0]);
+        if (!same) release_ticket(a.done, (int)ent[1], tk[1]);
+        OWNER_MARK(8);
+        OWNER_COUNT(11);
     }
+    if (cur >= 0) {
+        R.store(a.rel + (int64_t)cur * a.ld, n);
+        W.store(a.w + (int64_t)cur * a.ld, n);
+    }
+#ifdef KB2E_OWNER_PROF
+    pc.flush();
+#endif
 }
 
 
@@ -648,37 +940,6 @@ __global__ __launch_bounds__(256) void transr_compat_energy_kernel(RScoreArgs<T>
 
 // ---------------------------------------------------------- TransR phase B
 
-// Diagnostic build only (make prof): per-phase cycle accounting of the owner.
-#ifdef KB2E_OWNER_PROF
-constexpr int kProfOwners = 1024;
-__device__ unsigned long long g_owner_prof[kProfOwners][16];
-struct PhaseClock {
-    unsigned long long t, acc[16];
-    __device__ void start() {
-        for (int k = 0; k < 16; ++k) acc[k] = 0;
-        t = clock64();
-    }
-    __device__ void mark(int k) {
-        const unsigned long long n = clock64();
-        acc[k] += n - t;
-        t = n;
-    }
-    __device__ void count(int k) { acc[k] += 1; }
-    __device__ void flush() {
-        if (lane_id() == 0 && blockIdx.x < kProfOwners)
-            for (int k = 0; k < 16; ++k) atomicAdd(&g_owner_prof[blockIdx.x][k], acc[k]);
-    }
-};
-#define OWNER_PC_PARAM , PhaseClock& pc
-#define OWNER_PC_ARG , pc
-#define OWNER_MARK(k) pc.mark(k)
-#define OWNER_COUNT(k) pc.count(k)
-#else
-#define OWNER_PC_PARAM
-#define OWNER_PC_ARG
-#define OWNER_MARK(k)
-#define OWNER_COUNT(k)
-#endif
 
 // transRNorm (transr/trainer.cpp:35-64) on an entity row held in registers,
 // with the relation matrix W (n x ldl) in LDS and `abuf` (n) as broadcast
@@ -894,102 +1155,6 @@ __global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32
 // parallel by transr_desc_kernel, so the serial owner loop does one uniform
 // load per update.
 
-// Descriptor of update (kk, u) at key position p: 3 x uint4
-//   q0 = {kk, u | count << 2 | roles0 << 4 | roles1 << 8 | roles2 << 12, r, 0}
-//   q1 = {ent0, ent1, ent2, 0}      q2 = {tick0, tick1, tick2, 0}
-// count == 0 marks an inactive update.
-template <typename T>
-__global__ __launch_bounds__(256) void transr_desc_kernel(OwnerArgs<T> a, int32_t ne) {
-    const int pb0 = a.seg_start[a.batch_seg[a.batch]];
-    const int pb1 = a.seg_start[a.batch_seg[a.batch + 1]];
-    for (int p = pb0 + blockIdx.x * blockDim.x + threadIdx.x; p < pb1; p += gridDim.x * blockDim.x) {
-        const uint64_t key = a.keys[p];
-        if (a.kl.row_of(key) < ne) continue;  // entity events
-        uint4* out = a.desc + (int64_t)(p - pb0) * 3;
-        const int kk = a.kl.kk_of(key);
-        if (!a.act[kk]) {
-            out[0] = make_uint4((uint32_t)kk, 0u, 0u, 0u);
-            continue;
-        }
-        const UpdateIds d = decode_update(a, key, true);
-        uint32_t packed = (uint32_t)d.u | ((uint32_t)d.count << 2);
-        for (int q = 0; q < d.count; ++q) packed |= d.roles[q] << (4 + 4 * q);
-        out[0] = make_uint4((uint32_t)kk, packed, (uint32_t)d.r, 0u);
-        out[1] = make_uint4((uint32_t)d.ent[0], d.count > 1 ? (uint32_t)d.ent[1] : 0u,
-                            d.count > 2 ? (uint32_t)d.ent[2] : 0u, 0u);
-        out[2] = make_uint4(d.tick[0], d.count > 1 ? d.tick[1] : 0u, d.count > 2 ? d.tick[2] : 0u, 0u);
-    }
-}
-
-// Per owner: the active descriptors of its segment, in order, packed to the
-// front of the segment's slice (cdesc[(p0 - pb0) + i]), and their count.
-__global__ __launch_bounds__(256) void transr_compact_kernel(const int32_t* owner_seg, const int32_t* seg_start,
-                                                             const int32_t* batch_seg, int32_t batch, int32_t owners,
-                                                             const uint4* desc, uint4* cdesc, int32_t* ocount) {
-    __shared__ int wave_tot[4];
-    const int o = blockIdx.x;
-    const int seg = owner_seg[(int64_t)batch * owners + o];
-    if (seg < 0) {
-        if (threadIdx.x == 0) ocount[o] = 0;
-        return;
-    }
-    const int p0 = seg_start[seg], p1 = seg_start[seg + 1];
-    const int pb0 = seg_start[batch_seg[batch]];
-    const int base = p0 - pb0;
-    const int wv = threadIdx.x >> 6, l = lane_id();
-    int running = 0;
-    for (int chunk = p0; chunk < p1; chunk += 256) {
-        const int p = chunk + threadIdx.x;
-        uint4 q0{}, q1{}, q2{};
-        bool active = false;
-        if (p < p1) {
-            const uint4* d = desc + (int64_t)(p - pb0) * 3;
-            q0 = d[0];
-            active = ((q0.y >> 2) & 3u) != 0;
-            if (active) {
-                q1 = d[1];
-                q2 = d[2];
-            }
-        }
-        const uint64_t m = __ballot(active);
-        if (l == 0) wave_tot[wv] = __popcll(m);
-        __syncthreads();
-        int before = __popcll(m & ((1ull << l) - 1ull));
-        for (int k = 0; k < wv; ++k) before += wave_tot[k];
-        const int total = wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
-        if (active) {
-            uint4* out = cdesc + (int64_t)(base + running + before) * 3;
-            out[0] = q0;
-            out[1] = q1;
-            out[2] = q2;
-        }
-        running += total;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) ocount[o] = running;
-}
-
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-
-// Wait until done[e_q] == tick_q for every slot (polls issued together).
-__device__ __forceinline__ void wait_tickets3(const uint32_t* done, int count, const uint32_t* e, const uint32_t* tk,
-                                              uint32_t* err) {
-    uint32_t spins = 0;
-    for (;;) {
-        const uint32_t f0 = __hip_atomic_load((gu32*)(done + e[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t f1 = count > 1 ? __hip_atomic_load((gu32*)(done + e[1]), __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT) : tk[1];
-        const uint32_t f2 = count > 2 ? __hip_atomic_load((gu32*)(done + e[2]), __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT) : tk[2];
-        if (f0 == tk[0] && f1 == tk[1] && f2 == tk[2]) return;
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 26)) {
-            __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-    }
-}
-
 // LDS row stride of the W' copy: = 1 (mod 16) doubles, so lane j writing row
 // j and lane i reading column i are both (nearly) conflict-free.
 __host__ __device__ constexpr int transr_ldl(int nm) { return ((nm + 14) / 16) * 16 + 1; }
@@ -1102,9 +1267,9 @@ __global__ __launch_bounds__(64) void transr_owner_reg_kernel(OwnerArgs<T> a, co
     PhaseClock pc;
     pc.start();
 #endif
-    // software pipeline: descriptor of update it+1 and its x / d elements are
-    // loaded during update it.
-    uint4 n0{}, n1{}, n2{};
+    // software pipeline: descriptors run two updates ahead, the x / d
+    // elements of update it+1 are loaded during update it.
+    uint4 n0{}, n1{}, n2{}, f0{}, f1{}, f2{};
     T nxl = T(0), ndl = T(0);
     if (m > 0) {
         n0 = dl0[0];
@@ -1114,14 +1279,22 @@ __global__ __launch_bounds__(64) void transr_owner_reg_kernel(OwnerArgs<T> a, co
         nxl = row_lane ? a.xreal[xo + l] : T(0);
         ndl = row_lane ? a.scal[xo + l] : T(0);
     }
+    if (m > 1) {
+        f0 = dl0[3];
+        f1 = dl0[4];
+        f2 = dl0[5];
+    }
     for (int it = 0; it < m; ++it) {
         const uint4 q0 = n0, q1 = n1, q2 = n2;
         const T xl = nxl, dl = ndl;
-        if (it + 1 < m) {
-            const uint4* dn = dl0 + (int64_t)(it + 1) * 3;
-            n0 = dn[0];
-            n1 = dn[1];
-            n2 = dn[2];
+        n0 = f0;
+        n1 = f1;
+        n2 = f2;
+        if (it + 2 < m) {
+            const uint4* dn = dl0 + (int64_t)(it + 2) * 3;
+            f0 = dn[0];
+            f1 = dn[1];
+            f2 = dn[2];
         }
         const uint32_t packed = uni(q0.y);
         const int count = (int)((packed >> 2) & 3);

@@ -14,8 +14,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-PHASES = ["decode/switch", "wait tickets", "load rows", "rank-1 W", "deltas+r", "norms (r,h,t,W rows)",
-          "transRNorm check", "transRNorm iterate", "store+release"]
+PHASES = ["decode/switch", "wait tickets", "load rows", "rank-1 W | H: deltas", "deltas+r | H: norms",
+          "(unused)",
+          "transRNorm check | H: orth(r)", "transRNorm iterate | H: orth(h,t)", "store+release"]
 
 
 def child(args):
