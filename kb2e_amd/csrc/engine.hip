@@ -1002,6 +1002,15 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
             }
             std::fill(pr.begin(), pr.end(), 0ull);
             HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_owner_prof), pr.data(), pr.size() * 8));
+            unsigned long long fp[2][16];
+            HIPCHK(hipMemcpyFromSymbol(fp, HIP_SYMBOL(g_fold_prof), sizeof(fp)));
+            for (int g = 0; g < 2; ++g) {
+                fprintf(stderr, "fold_prof %d", g);
+                for (int k = 0; k < 16; ++k) fprintf(stderr, " %llu", fp[g][k]);
+                fprintf(stderr, "\n");
+            }
+            std::memset(fp, 0, sizeof(fp));
+            HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_fold_prof), fp, sizeof(fp)));
         }
 #endif
         if (loss) *loss = c->acc_loss;

@@ -158,6 +158,39 @@ __device__ __forceinline__ bool xbit(const uint64_t* words, int c, int k) {
     return (words[c * kVec + k] >> lane_id()) & 1ull;
 }
 
+// ---- diagnostic build only (make prof): per-phase cycle accounting
+#ifdef KB2E_OWNER_PROF
+constexpr int kProfOwners = 1024;
+__device__ unsigned long long g_owner_prof[kProfOwners][16];  // relation owners
+__device__ unsigned long long g_fold_prof[2][16];              // fold: [0] segments >= 512 events, [1] shorter
+struct PhaseClock {
+    unsigned long long t, acc[16];
+    __device__ void start() {
+        for (int k = 0; k < 16; ++k) acc[k] = 0;
+        t = clock64();
+    }
+    __device__ void mark(int k) {
+        const unsigned long long n = clock64();
+        acc[k] += n - t;
+        t = n;
+    }
+    __device__ void count(int k, unsigned long long v = 1) { acc[k] += v; }
+    __device__ void flush(unsigned long long* dst) {
+        if (lane_id() == 0 && dst)
+            for (int k = 0; k < 16; ++k) atomicAdd(&dst[k], acc[k]);
+    }
+};
+#define OWNER_PC_PARAM , PhaseClock& pc
+#define OWNER_PC_ARG , pc
+#define OWNER_MARK(k) pc.mark(k)
+#define OWNER_COUNT(k) pc.count(k)
+#else
+#define OWNER_PC_PARAM
+#define OWNER_PC_ARG
+#define OWNER_MARK(k)
+#define OWNER_COUNT(k)
+#endif
+
 // ---- event keys: [batch | row | kk | u | roles] (most to least significant)
 struct KeyLayout {
     int kk_bits, row_bits, batch_bits;

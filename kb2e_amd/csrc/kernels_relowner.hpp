@@ -324,37 +324,6 @@ __device__ __forceinline__ void orth_norm(RowReg<T, CH>& A, RowReg<T, CH>& Bv, i
     Bv.norm(n, false);
 }
 
-// Diagnostic build only (make prof): per-phase cycle accounting of the owner.
-#ifdef KB2E_OWNER_PROF
-constexpr int kProfOwners = 1024;
-__device__ unsigned long long g_owner_prof[kProfOwners][16];
-struct PhaseClock {
-    unsigned long long t, acc[16];
-    __device__ void start() {
-        for (int k = 0; k < 16; ++k) acc[k] = 0;
-        t = clock64();
-    }
-    __device__ void mark(int k) {
-        const unsigned long long n = clock64();
-        acc[k] += n - t;
-        t = n;
-    }
-    __device__ void count(int k) { acc[k] += 1; }
-    __device__ void flush() {
-        if (lane_id() == 0 && blockIdx.x < kProfOwners)
-            for (int k = 0; k < 16; ++k) atomicAdd(&g_owner_prof[blockIdx.x][k], acc[k]);
-    }
-};
-#define OWNER_PC_PARAM , PhaseClock& pc
-#define OWNER_PC_ARG , pc
-#define OWNER_MARK(k) pc.mark(k)
-#define OWNER_COUNT(k) pc.count(k)
-#else
-#define OWNER_PC_PARAM
-#define OWNER_PC_ARG
-#define OWNER_MARK(k)
-#define OWNER_COUNT(k)
-#endif
 
 // ---------------------------------------------------------- TransH phase B
 
@@ -763,7 +732,7 @@ __global__ __launch_bounds__(64) void transh_owner_kernel(OwnerArgs<T> a, const 
         W.store(a.w + (int64_t)cur * a.ld, n);
     }
 #ifdef KB2E_OWNER_PROF
-    pc.flush();
+    pc.flush(blockIdx.x < kProfOwners ? g_owner_prof[blockIdx.x] : nullptr);
 #endif
 }
 
@@ -1139,7 +1108,7 @@ __global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32
         if (l == 0) a.wtouched[cur] = stamp;
     }
 #ifdef KB2E_OWNER_PROF
-    pc.flush();
+    pc.flush(blockIdx.x < kProfOwners ? g_owner_prof[blockIdx.x] : nullptr);
 #endif
 }
 
@@ -1420,7 +1389,7 @@ __global__ __launch_bounds__(64) void transr_owner_reg_kernel(OwnerArgs<T> a, co
         if (l == 0) a.wtouched[cur] = stamp;
     }
 #ifdef KB2E_OWNER_PROF
-    pc.flush();
+    pc.flush(blockIdx.x < kProfOwners ? g_owner_prof[blockIdx.x] : nullptr);
 #endif
 }
 

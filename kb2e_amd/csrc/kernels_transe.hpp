@@ -136,130 +136,248 @@ struct FoldArgs {
 // m accumulates S_m = sum_j beta_j e_j.e_m, and one elementwise
 // materialisation v = A (v0 + sum beta_j e_j).  Same decisions as the
 // reference; values agree to a few ulps per chunk.
-// 1/sqrt(x) to ~full FP64 precision: hardware estimate + two Newton steps.
+// 1/sqrt(x) to ~full FP64 precision: hardware estimate (rel. error ~5e-8 on
+// gfx950, tools/diag/rsq_accuracy.hip) + one third-order correction:
+// 1/sqrt(x) = y (1 - r)^-1/2 = y (1 + r/2 + 3r^2/8 + O(r^3)), r = 1 - x y^2.
+// 5 dependent operations instead of the 8 of two Newton steps.
 __device__ __forceinline__ double rsqrt_nr(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-    y = y * (1.5 - 0.5 * x * y * y);
-    y = y * (1.5 - 0.5 * x * y * y);
-    return y;
+    const double y = __builtin_amdgcn_rsq(x);
+    const double xy = x * y;
+    const double r = fma(-xy, y, 1.0);
+    const double p = fma(r, 0.375, 0.5);
+    return fma(y, r * p, y);
 }
+
+// Per-wave LDS of the recurrence path.
+template <int CH>
+struct GramLds {
+    double v[CH * kWave * kVec];   // v0 of the chunk (broadcast reads)
+    uint64_t x[kWave][2 * CH];     // sign words of the chunk's active events, compacted
+    double4 ev[kWave];             // per active event: {lr v0.x, 2 s, |e|^2, s lr^2}
+    int s[kWave];                  // s of the active events, compacted
+};
+
+// Events of one chunk, one per lane: s (sign of e), number of norms, x words.
+template <int CH>
+struct ChunkEvents {
+    int sgn, nn;
+    uint64_t xw[2 * CH];
+};
+
+// Raw loads of a chunk's event data (decoded later, so issuing them does not
+// wait for them).
+template <typename T, int CH>
+struct ChunkLoads {
+    uint64_t key;
+    uint32_t act;
+    uint64_t xw[2 * CH];
+    __device__ __forceinline__ void issue(const FoldArgs<T>& a, bool valid) {
+        act = 0;
+#pragma unroll
+        for (int q = 0; q < 2 * CH; ++q) xw[q] = 0ull;
+        if (valid) {
+            const int kk = a.kl.kk_of(key);
+            const int u = (int)((key >> 3) & 1);
+            act = a.act[kk];
+#pragma unroll
+            for (int q = 0; q < 2 * CH; ++q) xw[q] = a.xbits[((int64_t)kk * 2 + u) * a.nw + q];
+        }
+    }
+    __device__ __forceinline__ ChunkEvents<CH> decode(bool valid, bool is_rel) const {
+        ChunkEvents<CH> ev;
+        ev.sgn = 0;
+        ev.nn = 0;
+#pragma unroll
+        for (int q = 0; q < 2 * CH; ++q) ev.xw[q] = 0ull;
+        if (valid && act) {
+            // e = s * lr * x: relation and head rows take -d, tail rows +d,
+            // d = (neg update ? +1 : -1) * lr * x (transe/trainer.cpp:26, 38-40)
+            const int us = ((key >> 3) & 1) ? 1 : -1;
+            const uint32_t roles = (uint32_t)(key & 7);
+            if (is_rel) {
+                ev.sgn = -us;
+                ev.nn = 1;
+            } else {
+                const bool hd = roles & kRoleHead, tl = roles & kRoleTail;
+                ev.sgn = (hd && tl) ? 0 : (hd ? -us : us);
+                ev.nn = (hd ? 1 : 0) + (tl ? 1 : 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 2 * CH; ++q) ev.xw[q] = xw[q];
+        }
+        return ev;
+    }
+};
 
 template <typename T, int CH>
 __device__ void fold_segment_gram(const FoldArgs<T>& a, int p0, int p1, bool is_rel, RowReg<T, CH>& V,
-                                  double* lds_v, bool& dirty) {
+                                  GramLds<CH>* L, bool& dirty) {
+    constexpr int NW = 2 * CH;
     const int l = lane_id();
     const double lr = a.lr;
     const double lr2 = lr * lr;
     const double eps = lr2 * (double)a.n;
+    // first chunk: synchronous
+    ChunkLoads<T, CH> ld;
+    ld.key = p0 + l < p1 ? a.keys[p0 + l] : 0ull;
+    ld.issue(a, p0 + l < p1);
+    ChunkEvents<CH> ev = ld.decode(p0 + l < p1, is_rel);
+#ifdef KB2E_OWNER_PROF
+    PhaseClock pc;
+    pc.start();
+#endif
     for (int base = p0; base < p1; base += kWave) {
-        const int cnt = min(kWave, p1 - base);
-        uint64_t xw[2 * CH];
-        int sgn = 0, nn = 0;
+        const int nbase = base + kWave;
+        const bool nvalid = nbase + l < p1;
+        ChunkLoads<T, CH> nld;
+        nld.key = nvalid ? a.keys[nbase + l] : 0ull;  // level 1 of the next chunk
+        const uint64_t m_act = __ballot(ev.nn > 0);
+        if (m_act) {
+            dirty = true;
+            // Active events only, in order, moved to lanes 0..cnt-1 (inactive
+            // samples leave the row untouched).
+            const int cnt = __popcll(m_act);
+            const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m_act >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m_act, 0u));
+            if (ev.nn > 0) {
 #pragma unroll
-        for (int q = 0; q < 2 * CH; ++q) xw[q] = 0ull;
-        if (l < cnt) {
-            const uint64_t key = a.keys[base + l];
-            const int kk = a.kl.kk_of(key);
-            if (a.act[kk]) {
-                const int u = (int)((key >> 3) & 1);
-                const uint32_t roles = (uint32_t)(key & 7);
-                // e = s * lr * x: relation and head rows take -d, tail rows +d,
-                // d = (neg update ? +1 : -1) * lr * x (transe/trainer.cpp:26, 38-40)
-                const int us = u ? 1 : -1;
-                if (is_rel) {
-                    sgn = -us;
-                    nn = 1;
-                } else {
-                    const bool hd = roles & kRoleHead, tl = roles & kRoleTail;
-                    sgn = (hd && tl) ? 0 : (hd ? -us : us);
-                    nn = (hd ? 1 : 0) + (tl ? 1 : 0);
-                }
-#pragma unroll
-                for (int q = 0; q < 2 * CH; ++q) xw[q] = a.xbits[((int64_t)kk * 2 + u) * a.nw + q];
+                for (int q = 0; q < NW; ++q) L->x[pos][q] = ev.xw[q];
+                L->s[pos] = ev.sgn;
             }
-        }
-        const uint64_t m_act = __ballot(nn > 0);
-        if (!m_act) continue;
-        const uint64_t m_sgn = __ballot(sgn != 0), m_n2 = __ballot(nn == 2);
-        dirty = true;
-        // p_m = s_m lr (v0 . x_m): v0 to LDS, lane m walks the row
-#pragma unroll
-        for (int c = 0; c < CH; ++c)
-#pragma unroll
-            for (int k = 0; k < kVec; ++k) {
-                const int e = c * (kWave * kVec) + l * kVec + k;
-                if (e < a.n) lds_v[e] = (double)V.v[c][k];
-            }
-        wave_lds_sync();
-        double pm = 0;
-        for (int e = 0; e < a.n; ++e) {
-            const int c = e / (kWave * kVec), r = e % (kWave * kVec);
-            const double v = lds_v[e];
-            pm += ((xw[c * kVec + (r & 1)] >> (r >> 1)) & 1ull) ? v : -v;
-        }
-        pm *= (double)sgn * lr;
-        // e_k . e_m / lr^2 = s_k s_m (n - 2 popcount(bits_k ^ bits_m)), for every k (lane m)
-        int gk[kWave];
-#pragma unroll
-        for (int k = 0; k < kWave; ++k) {
-            uint32_t dis = 0;
-#pragma unroll
-            for (int q = 0; q < 2 * CH; ++q) dis += (uint32_t)__popcll(xw[q] ^ readlane_u64(xw[q], k));
-            gk[k] = readlane_i32(sgn, k) * sgn * (a.n - 2 * (int)dis);
-        }
-        double N = (double)V.sumsq();
-        double A = 1.0, invA = 1.0, S = 0.0, beta_mine = 0.0;
-#pragma unroll
-        for (int k = 0; k < kWave; ++k) {
-            if (!((m_act >> k) & 1ull)) continue;  // wave-uniform
-            const double z2 = N + 2.0 * A * (readlane_f(pm, k) + readlane_f(S, k)) +
-                              (((m_sgn >> k) & 1ull) ? eps : 0.0);
-            beta_mine = (l == k) ? invA : beta_mine;
-            S += invA * lr2 * (double)gk[k];
-            double nz = z2;
-            if (z2 > 1.0) {  // common::norm: len > 1 -> v /= len
-                const double y = rsqrt_nr(z2);
-                A *= y;
-                invA *= z2 * y;
-                nz = z2 * y * y;
-            }
-            if (((m_n2 >> k) & 1ull) && nz > 1.0) {  // second role of the same row
-                const double y = rsqrt_nr(nz);
-                A *= y;
-                invA *= nz * y;
-                nz = nz * y * y;
-            }
-            N = nz;
-        }
-        // v = A * (v0 + sum_k beta_k s_k lr x_k)
-        double u[CH][kVec];
-#pragma unroll
-        for (int c = 0; c < CH; ++c)
-#pragma unroll
-            for (int k = 0; k < kVec; ++k) u[c][k] = (double)V.v[c][k];
-#pragma unroll
-        for (int k = 0; k < kWave; ++k) {
-            if (!((m_sgn >> k) & 1ull)) continue;
-            const double w = readlane_f(beta_mine, k) * (double)readlane_i32(sgn, k) * lr;
-            uint64_t words[2 * CH];
-#pragma unroll
-            for (int q = 0; q < 2 * CH; ++q) words[q] = readlane_u64(xw[q], k);
+            // v0 (zero padding included) to LDS
 #pragma unroll
             for (int c = 0; c < CH; ++c)
 #pragma unroll
-                for (int kv = 0; kv < kVec; ++kv) u[c][kv] += xbit(words, c, kv) ? w : -w;
+                for (int k = 0; k < kVec; ++k) L->v[c * (kWave * kVec) + l * kVec + k] = (double)V.v[c][k];
+            wave_lds_sync();
+            uint64_t xw[NW];
+#pragma unroll
+            for (int q = 0; q < NW; ++q) xw[q] = l < cnt ? L->x[l][q] : 0ull;
+            const int sg = l < cnt ? L->s[l] : 0;
+            // pm_m = lr (v0 . x_m): element pair (128c + 2j, +1) has sign bits j
+            // of words 2c and 2c + 1; four partial sums, groups of 8 pairs past
+            // the row's end skipped.
+            double pq[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int c = 0; c < CH; ++c)
+#pragma unroll
+                for (int j0 = 0; j0 < kWave; j0 += 8) {
+                    if (c * (kWave * kVec) + 2 * j0 >= a.n) continue;  // wave-uniform
+#pragma unroll
+                    for (int j = j0; j < j0 + 8; ++j) {
+                        const double2 vv = *reinterpret_cast<const double2*>(&L->v[c * (kWave * kVec) + 2 * j]);
+                        const bool b0 = (xw[c * kVec] >> j) & 1ull, b1 = (xw[c * kVec + 1] >> j) & 1ull;
+                        pq[(2 * j) & 3] += b0 ? vv.x : -vv.x;
+                        pq[(2 * j + 1) & 3] += b1 ? vv.y : -vv.y;
+                    }
+                }
+            const double sd = (double)sg;
+            L->ev[l] = make_double4(((pq[0] + pq[1]) + (pq[2] + pq[3])) * lr, 2.0 * sd, sg != 0 ? eps : 0.0,
+                                    sd * lr2);
+            wave_lds_sync();
+            nld.issue(a, nvalid);  // level 2 of the next chunk: in flight during the chain
+            OWNER_MARK(1);
+            // The chain, one active event per step, branch free.  With
+            // e_k = s_k lr x_k, write v = A (v0 + sum_{j<k} beta_j e_j); then
+            //   |v + e_k|^2 = N + 2 A s_k (lr v0.x_k + T_k) + |e_k|^2,
+            //   T_m = sum_{j<m} beta_j s_j lr^2 (n - 2 popcount(bits_j ^ bits_m)),
+            // which lane m accumulates one event at a time (x_j . x_m from the
+            // sign words).  Only z2 -> rsqrt -> scale -> next z2 is serial: the
+            // next event's 2 A s (pm + T) is formed from values known at the
+            // start of a step, and a renormalised row's squared length is
+            // tracked as exactly 1 (so a row used as head and tail, e = 0 with
+            // two norms, needs one step).  Event k+1's table entry and sign
+            // words are read from LDS one step ahead.
+            double N = (double)V.sumsq();
+            double A = 1.0, invA = 1.0, Tm = 0.0, beta_mine = 0.0;
+            double f = 1.0;  // scale applied by the previous step
+            double4 e1 = L->ev[0];
+            double P = e1.y * e1.x;  // 2 A_{-1} s_0 (pm_0 + T_0), A_{-1} = 1, T_0 = 0
+            uint64_t x1[NW];
+#pragma unroll
+            for (int q = 0; q < NW; ++q) x1[q] = L->x[0][q];
+            auto tcoef = [&](const uint64_t (&xk)[NW]) {
+                uint32_t dis = 0;
+#pragma unroll
+                for (int q = 0; q < NW; ++q) dis += (uint32_t)__popcll(xw[q] ^ xk[q]);
+                return (double)(a.n - 2 * (int)dis);
+            };
+            double tk = tcoef(x1);
+            double4 ek = e1;
+#pragma unroll 1
+            for (int k = 0; k < cnt; ++k) {
+                const int k1 = k + 1 < kWave ? k + 1 : k;
+                e1 = L->ev[k1];
+#pragma unroll
+                for (int q = 0; q < NW; ++q) x1[q] = L->x[k1][q];
+                const double z2 = fma(f, P, N + ek.z);
+                const bool big = z2 > 1.0;  // common::norm: len > 1 -> v /= len
+                const double y = rsqrt_nr(z2);
+                // off the serial path
+                A *= f;
+                beta_mine = (l == k) ? invA : beta_mine;
+                Tm = fma(invA * ek.w, tk, Tm);
+                const double Pn = (A * e1.y) * (e1.x + readlane_f(Tm, k1));
+                tk = tcoef(x1);
+                // serial tail
+                f = big ? y : 1.0;
+                invA = big ? invA * (z2 * y) : invA;
+                N = big ? 1.0 : z2;
+                P = Pn;
+                ek = e1;
+            }
+            A *= f;
+#ifdef KB2E_OWNER_PROF
+            pc.mark(2);
+            pc.count(10, (unsigned long long)cnt);
+            pc.count(11, (unsigned long long)cnt);
+#endif
+            // v = A (v0 + sum_k w_k x_k), w_k = beta_k s_k lr.  Event k's sign
+            // word for element parity kv of chunk c is itself the lane mask
+            // (bit l <-> lane l) that picks +w_k or -w_k.
+            const double w_mine = beta_mine * (double)sg * lr;
+            double u[CH][kVec];
+#pragma unroll
+            for (int c = 0; c < CH; ++c)
+#pragma unroll
+                for (int k = 0; k < kVec; ++k) u[c][k] = (double)V.v[c][k];
+#pragma unroll 1
+            for (int k = 0; k < cnt; ++k) {
+                const double w = readlane_f(w_mine, k);
+                const uint32_t wlo = (uint32_t)__double_as_longlong(w);
+                const uint32_t whi = (uint32_t)(__double_as_longlong(w) >> 32);
+                const uint32_t whn = whi ^ 0x80000000u;  // -w differs in the sign bit only
+#pragma unroll
+                for (int c = 0; c < CH; ++c)
+#pragma unroll
+                    for (int kv = 0; kv < kVec; ++kv) {
+                        const uint64_t word = readlane_u64(xw[c * kVec + kv], k);
+                        uint32_t hi;
+                        asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(hi) : "v"(whn), "v"(whi), "s"(word));
+                        u[c][kv] += __longlong_as_double(((long long)hi << 32) | wlo);
+                    }
+            }
+#pragma unroll
+            for (int c = 0; c < CH; ++c)
+#pragma unroll
+                for (int k = 0; k < kVec; ++k) V.v[c][k] = elem_valid(c, k, a.n) ? (T)(A * u[c][k]) : T(0);
+            wave_lds_sync();
+            OWNER_MARK(3);
+        } else {
+            nld.issue(a, nvalid);
         }
-#pragma unroll
-        for (int c = 0; c < CH; ++c)
-#pragma unroll
-            for (int k = 0; k < kVec; ++k) V.v[c][k] = elem_valid(c, k, a.n) ? (T)(A * u[c][k]) : T(0);
-        wave_lds_sync();
+        ev = nld.decode(nvalid, is_rel);
+        OWNER_MARK(4);
+        OWNER_COUNT(12);
     }
+#ifdef KB2E_OWNER_PROF
+    pc.flush(g_fold_prof[p1 - p0 >= 512 ? 0 : 1]);
+#endif
 }
 
 template <typename T, int CH, bool L1>
 __global__ __launch_bounds__(256) void transe_fold_kernel(FoldArgs<T> a) {
-    __shared__ double lds_v[4 * CH * kWave * kVec];  // one row per wave (gram path)
+    __shared__ GramLds<CH> glds[4];  // one per wave (recurrence path)
     const int s0 = a.batch_seg[a.batch], s1 = a.batch_seg[a.batch + 1];
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -274,7 +392,7 @@ __global__ __launch_bounds__(256) void transe_fold_kernel(FoldArgs<T> a) {
         V.load(ptr, a.n);
         bool dirty = false;
         if (L1 && a.gram_min > 0 && p1 - p0 >= a.gram_min) {
-            fold_segment_gram<T, CH>(a, p0, p1, is_rel, V, lds_v + (threadIdx.x >> 6) * (CH * kWave * kVec), dirty);
+            fold_segment_gram<T, CH>(a, p0, p1, is_rel, V, &glds[threadIdx.x >> 6], dirty);
             if (dirty) V.store(ptr, a.n);
             continue;
         }

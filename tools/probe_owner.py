@@ -24,7 +24,7 @@ def child(args):
     import time
     from kb2e_amd import data
     from kb2e_amd.engine import Engine
-    ds = data.synthetic("fb15k", seed=0)
+    ds = data.synthetic("fb15k", seed=0, relation_zipf=args.zipf)
     eng = Engine(args.model, args.dim, ds.num_entities, ds.num_relations, rate=0.001, method=1, distance=0,
                  batches=100, seed=7, precision=args.precision)
     eng.upload_triples(ds.train)
@@ -49,13 +49,29 @@ def main():
     ap.add_argument("--batches", type=int, default=20)
     ap.add_argument("--precision", type=int, default=64)
     ap.add_argument("--child", action="store_true")
+    ap.add_argument("--zipf", type=float, default=None, help="relation Zipf exponent of the synthetic data")
     args = ap.parse_args()
     if args.child:
         return child(args)
     cmd = [sys.executable, __file__, "--child", "--model", args.model, "--dim", str(args.dim), "--batches",
            str(args.batches), "--precision", str(args.precision)]
+    if args.zipf is not None:
+        cmd += ["--zipf", str(args.zipf)]
     res = subprocess.run(cmd, capture_output=True, text=True)
     print(res.stdout)
+    if args.model == "E":
+        FOLD = ["first chunk", "LDS + p_m", "chain", "materialise", "next chunk decode"]
+        for line in res.stderr.splitlines():
+            if line.startswith("fold_prof"):
+                f = [int(x) for x in line.split()[1:]]
+                g, v = f[0], f[1:]
+                ev, steps, chunks = max(1, v[10]), max(1, v[11]), max(1, v[12])
+                print(f"{'segments >= 512 events' if g == 0 else 'shorter segments'}: events {v[10]} "
+                      f"steps {v[11]} chunks {v[12]}")
+                for k, name in enumerate(FOLD):
+                    print(f"  {name:20s} {v[k] / ev:8.0f} cycles/event  {v[k] / chunks:9.0f} cycles/chunk")
+                print(f"  chain per step {v[2] / steps:8.0f} cycles")
+        return
     rows = {}
     for line in res.stderr.splitlines():
         if line.startswith("owner_prof"):
