@@ -29,6 +29,7 @@
 #include "kernels_common.hpp"
 #include "kernels_index.hpp"
 #include "kernels_transe.hpp"
+#include "kernels_transe_long.hpp"
 #include "kernels_relowner.hpp"
 #include "kernels_sampler.hpp"
 #include "kernels_eval.hpp"
@@ -146,6 +147,10 @@ struct kb2e_ctx {
     int num_cus = 256;
     uint32_t batch_stamp = 0;
     int32_t gram_min = 48;  // KB2E_GRAM_MIN: fold segments this long use the scalar recurrence (0 = off)
+    int32_t long_min = 192;  // KB2E_FOLD_LONG: segments this long take the 4-wave fold (0 = off; L1 only)
+    hipStream_t fold_stream = nullptr;  // the long-segment fold runs beside the per-row fold
+    hipEvent_t ev_fold_a = nullptr, ev_fold_b = nullptr;
+    DevBuf long_list, long_count;
     // stats
     DevBuf stats;  // double loss, double active (reduced)
     double acc_loss = 0;
@@ -174,6 +179,9 @@ struct kb2e_ctx {
         if (ev_sampled) (void)hipEventDestroy(ev_sampled);
         if (ev_epoch_done) (void)hipEventDestroy(ev_epoch_done);
         if (side_stream) (void)hipStreamDestroy(side_stream);
+        if (fold_stream) (void)hipStreamDestroy(fold_stream);
+        if (ev_fold_a) (void)hipEventDestroy(ev_fold_a);
+        if (ev_fold_b) (void)hipEventDestroy(ev_fold_b);
         for (auto e : event_pool) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -197,14 +205,19 @@ struct kb2e_ctx {
     // Bracket a launch with events on the engine stream (when profiling).
     template <class F>
     void timed(const char* name, F&& f) {
+        timed_on(stream, name, f);
+    }
+    // ... or on another stream that the engine stream later waits for.
+    template <class F>
+    void timed_on(hipStream_t st, const char* name, F&& f) {
         if (!prof) {
             f();
             return;
         }
         hipEvent_t a = get_event(), b = get_event();
-        HIPCHK(hipEventRecord(a, stream));
+        HIPCHK(hipEventRecord(a, st));
         f();
-        HIPCHK(hipEventRecord(b, stream));
+        HIPCHK(hipEventRecord(b, st));
         pending.push_back({name, a, b});
         if (pending.size() > 4096) flush_timers();
     }
@@ -537,14 +550,45 @@ void run_batch_transe(kb2e_ctx* c, int64_t b) {
     fa.xbits = sa.xbits;
     fa.xreal = sa.xreal;
     fa.gram_min = c->gram_min;
+    const bool use_long = l1 && c->long_min > 0 && c->gram_min > 0;
+    fa.long_min = use_long ? c->long_min : 0;
     // Enough waves for every touched row of a batch (<= 6 B segments).
     const int64_t max_seg = std::min<int64_t>(c->B * 6, (int64_t)c->cfg.num_entities + c->cfg.num_relations);
     const int fgrid = (int)std::max<int64_t>(1, std::min<int64_t>((max_seg + 3) / 4, 4096));
+    if (use_long) {
+        // long segments: one 4-wave workgroup each, on the fold stream, beside the per-row fold
+        long_segments_kernel<<<1, 1024, 0, c->stream>>>(fa.seg_start, fa.batch_seg, fa.batch, c->long_min,
+                                                        c->long_list.as<int32_t>(), c->long_count.as<int32_t>());
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c->ev_fold_a, c->stream));
+        HIPCHK(hipStreamWaitEvent(c->fold_stream, c->ev_fold_a, 0));
+        c->timed_on(c->fold_stream, "fold_long", [&] {
+            transe_fold_long_kernel<T, CH><<<128, 256, fold_long_lds_bytes<T, CH>(), c->fold_stream>>>(
+                fa, c->long_list.as<int32_t>(), c->long_count.as<int32_t>());
+            HIPCHK(hipGetLastError());
+        });
+        HIPCHK(hipEventRecord(c->ev_fold_b, c->fold_stream));
+    }
     c->timed("fold", [&] {
         if (l1) transe_fold_kernel<T, CH, true><<<fgrid, 256, 0, c->stream>>>(fa);
         else transe_fold_kernel<T, CH, false><<<fgrid, 256, 0, c->stream>>>(fa);
         HIPCHK(hipGetLastError());
     });
+    if (use_long) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_fold_b, 0));
+}
+
+template <typename K>
+void allow_lds(K kernel, size_t bytes) {
+    (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+void prepare_fold_long_kernels() {
+    allow_lds(transe_fold_long_kernel<double, 1>, fold_long_lds_bytes<double, 1>());
+    allow_lds(transe_fold_long_kernel<double, 2>, fold_long_lds_bytes<double, 2>());
+    allow_lds(transe_fold_long_kernel<double, 4>, fold_long_lds_bytes<double, 4>());
+    allow_lds(transe_fold_long_kernel<float, 1>, fold_long_lds_bytes<float, 1>());
+    allow_lds(transe_fold_long_kernel<float, 2>, fold_long_lds_bytes<float, 2>());
+    allow_lds(transe_fold_long_kernel<float, 4>, fold_long_lds_bytes<float, 4>());
 }
 
 template <typename T>
@@ -654,6 +698,8 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     c->nb = g.num_batches;
     c->S = c->B * c->nb;
     if (c->B < 1) throw std::invalid_argument("fewer training triples than batches");
+    c->long_list.alloc((size_t)c->B * c->slots * 4);
+    c->long_count.alloc(16);
     for (int q = 0; q < 2; ++q) {
         c->si_[q].alloc(c->S * 4);
         c->sj_[q].alloc(c->S * 4);
@@ -768,12 +814,17 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
         HIPCHK(hipSetDevice(g.device));
         HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&c->fold_stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_fold_a, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_fold_b, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->ev_sampled, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->ev_epoch_done, hipEventDisableTiming));
         HIPCHK(hipEventRecord(c->ev_epoch_done, c->stream));
         HIPCHK(hipDeviceGetAttribute(&c->num_cus, hipDeviceAttributeMultiprocessorCount, g.device));
         prepare_relowner_kernels();
+        prepare_fold_long_kernels();
         if (const char* gm = getenv("KB2E_GRAM_MIN")) c->gram_min = atoi(gm);
+        if (const char* lm = getenv("KB2E_FOLD_LONG")) c->long_min = atoi(lm);
         const char* hs = getenv("KB2E_HOST_SAMPLER");
         c->host_sampler = hs && hs[0] == '1';
         setup_buffers(c.get());
@@ -1011,6 +1062,11 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
             }
             std::memset(fp, 0, sizeof(fp));
             HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_fold_prof), fp, sizeof(fp)));
+            HIPCHK(hipMemcpyFromSymbol(fp[0], HIP_SYMBOL(g_long_prof), sizeof(fp[0])));
+            fprintf(stderr, "long_prof");
+            for (int k = 0; k < 16; ++k) fprintf(stderr, " %llu", fp[0][k]);
+            fprintf(stderr, "\n");
+            HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_long_prof), fp[1], sizeof(fp[1])));
         }
 #endif
         if (loss) *loss = c->acc_loss;

@@ -75,6 +75,19 @@ __device__ __forceinline__ T div_markstein(T a, T b, T y) {
     return fma(r, y, q);
 }
 
+// Keep a value in registers from here on: an empty asm that "modifies" it
+// stops the compiler from re-loading it later from LDS (which would turn a
+// one-step-ahead prefetch back into a load-and-wait at the point of use).
+__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(float& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(uint64_t& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(double4& x) {
+    pin(x.x);
+    pin(x.y);
+    pin(x.z);
+    pin(x.w);
+}
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 // Order LDS traffic between the lanes of ONE wave (no workgroup barrier: the
@@ -163,6 +176,7 @@ __device__ __forceinline__ bool xbit(const uint64_t* words, int c, int k) {
 constexpr int kProfOwners = 1024;
 __device__ unsigned long long g_owner_prof[kProfOwners][16];  // relation owners
 __device__ unsigned long long g_fold_prof[2][16];              // fold: [0] segments >= 512 events, [1] shorter
+__device__ unsigned long long g_long_prof[16];                 // 4-wave long-segment fold
 struct PhaseClock {
     unsigned long long t, acc[16];
     __device__ void start() {

@@ -120,6 +120,7 @@ struct FoldArgs {
     const uint64_t* xbits;  // [B][2][nw]
     const T* xreal;         // [B][2][ld]
     int32_t gram_min;       // segments at least this long take the scalar-recurrence path (0: never)
+    int32_t long_min;       // segments at least this long are left to transe_fold_long_kernel (0: none)
 };
 
 // ---- long L1 segments: the renormalisation recurrence on scalars ----------
@@ -291,25 +292,29 @@ __device__ void fold_segment_gram(const FoldArgs<T>& a, int p0, int p1, bool is_
             double N = (double)V.sumsq();
             double A = 1.0, invA = 1.0, Tm = 0.0, beta_mine = 0.0;
             double f = 1.0;  // scale applied by the previous step
-            double4 e1 = L->ev[0];
-            double P = e1.y * e1.x;  // 2 A_{-1} s_0 (pm_0 + T_0), A_{-1} = 1, T_0 = 0
-            uint64_t x1[NW];
-#pragma unroll
-            for (int q = 0; q < NW; ++q) x1[q] = L->x[0][q];
+            // event table entries read two steps ahead, sign words one step
             auto tcoef = [&](const uint64_t (&xk)[NW]) {
                 uint32_t dis = 0;
 #pragma unroll
                 for (int q = 0; q < NW; ++q) dis += (uint32_t)__popcll(xw[q] ^ xk[q]);
                 return (double)(a.n - 2 * (int)dis);
             };
+            double4 ek = L->ev[0], e1 = L->ev[1];
+            double P = ek.y * ek.x;  // 2 A_{-1} s_0 (pm_0 + T_0), A_{-1} = 1, T_0 = 0
+            uint64_t x1[NW];
+#pragma unroll
+            for (int q = 0; q < NW; ++q) x1[q] = L->x[0][q];
             double tk = tcoef(x1);
-            double4 ek = e1;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) x1[q] = L->x[1][q];
 #pragma unroll 1
             for (int k = 0; k < cnt; ++k) {
                 const int k1 = k + 1 < kWave ? k + 1 : k;
-                e1 = L->ev[k1];
+                const int k2 = k + 2 < kWave ? k + 2 : kWave - 1;
+                double4 e2 = L->ev[k2];
+                uint64_t x2[NW];
 #pragma unroll
-                for (int q = 0; q < NW; ++q) x1[q] = L->x[k1][q];
+                for (int q = 0; q < NW; ++q) x2[q] = L->x[k2][q];
                 const double z2 = fma(f, P, N + ek.z);
                 const bool big = z2 > 1.0;  // common::norm: len > 1 -> v /= len
                 const double y = rsqrt_nr(z2);
@@ -325,6 +330,14 @@ __device__ void fold_segment_gram(const FoldArgs<T>& a, int p0, int p1, bool is_
                 N = big ? 1.0 : z2;
                 P = Pn;
                 ek = e1;
+                e1 = e2;
+                pin(ek);
+                pin(e1);
+#pragma unroll
+                for (int q = 0; q < NW; ++q) {
+                    x1[q] = x2[q];
+                    pin(x1[q]);
+                }
             }
             A *= f;
 #ifdef KB2E_OWNER_PROF
@@ -385,6 +398,7 @@ __global__ __launch_bounds__(256) void transe_fold_kernel(FoldArgs<T> a) {
     // Relation rows sort last and carry the longest event chains: start them first.
     for (int s = s1 - 1 - wave; s >= s0; s -= nwaves) {
         const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
+        if (a.long_min > 0 && p1 - p0 >= a.long_min) continue;  // transe_fold_long_kernel's
         const int row = a.kl.row_of(a.keys[p0]);
         const bool is_rel = row >= a.ne;
         T* ptr = is_rel ? a.rel + (int64_t)(row - a.ne) * a.ld : a.ent + (int64_t)row * a.ld;

@@ -71,6 +71,14 @@ def main():
                 for k, name in enumerate(FOLD):
                     print(f"  {name:20s} {v[k] / ev:8.0f} cycles/event  {v[k] / chunks:9.0f} cycles/chunk")
                 print(f"  chain per step {v[2] / steps:8.0f} cycles")
+            if line.startswith("long_prof"):
+                v = [int(x) for x in line.split()[1:]]
+                ev, phases = max(1, v[10]), max(1, v[12])
+                print(f"4-wave long fold: events {v[10]}, wave-phases {v[12]} ({v[12] / 4:.0f} chunk phases)")
+                for wv, name in enumerate(["chain", "materialise+P0", "decode+t", "cross t+table"]):
+                    print(f"  wave {wv} {name:16s} work {v[wv] / (phases / 4):8.0f} cycles/phase  "
+                          f"barrier wait {v[4 + wv] / (phases / 4):8.0f}")
+                print(f"  chain per event {v[0] / ev:8.0f} cycles")
         return
     rows = {}
     for line in res.stderr.splitlines():
