@@ -50,46 +50,23 @@ def algorithmic_bytes_per_sample(model, n, s, active_frac):
     return full, 20 + (n * n + 5 * n) * s, active_frac * (2 * n * n + 10 * n) * s
 
 
-def _epoch_stamps(cmd, limit_s):
-    """Run the reference on one core under a pseudo-terminal (so its stdout is
-    line-buffered, as in a shell) and time-stamp each `Epoch:` line."""
-    import pty
-    import select
+def _ref_epoch_seconds(cmd, e1, e2, limit_s):
+    """Seconds per epoch of the reference binary on one core:
+    (wall(e2 epochs) - wall(e1 epochs)) / (e2 - e1), so data loading,
+    initialisation and writing the output files cancel out."""
+    cpu = min(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
 
-    master, slave = pty.openpty()
-    try:
-        os.sched_setaffinity(0, {min(os.sched_getaffinity(0))})
-        pin = True
-    except (AttributeError, OSError):
-        pin = False
-    p = subprocess.Popen(cmd, stdout=slave, stderr=subprocess.DEVNULL, close_fds=True)
-    os.close(slave)
-    stamps, buf, t0 = [], b"", time.time()
-    try:
-        while len(stamps) < 4 and time.time() - t0 < limit_s:
-            r, _, _ = select.select([master], [], [], 1.0)
-            if not r:
-                if p.poll() is not None:
-                    break
-                continue
-            try:
-                chunk = os.read(master, 4096)
-            except OSError:
-                break
-            if not chunk:
-                break
-            buf += chunk
-            while b"\n" in buf:
-                line, buf = buf.split(b"\n", 1)
-                if line.startswith(b"Epoch:"):
-                    stamps.append(time.time())
-    finally:
-        p.kill()
-        p.wait()
-        os.close(master)
-        if pin:
-            os.sched_setaffinity(0, set(range(os.cpu_count() or 1)))
-    return stamps
+    def pin():
+        if cpu is not None:
+            os.sched_setaffinity(0, {cpu})
+
+    wall = []
+    for e in (e1, e2):
+        t0 = time.perf_counter()
+        subprocess.run(cmd + ["--epochs", str(e)], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                       timeout=limit_s, preexec_fn=pin, check=True)
+        wall.append(time.perf_counter() - t0)
+    return (wall[1] - wall[0]) / (e2 - e1)
 
 
 def cpu_baseline(cfg_name, ds, budget_s=25.0):
@@ -99,17 +76,30 @@ def cpu_baseline(cfg_name, ds, budget_s=25.0):
     model, shape, dim, method, distance, rate = CONFIGS[cfg_name]
     binary = os.path.join(ROOT, "oracle", "_ref", {"E": "trainTransE", "H": "trainTransH", "R": "trainTransR"}[model])
     S = (len(ds.train) // 100) * 100
-    if os.path.exists(binary) and model == "E":
+    if os.path.exists(binary):
+        # (e1, e2) epochs: wall(e2) - wall(e1) keeps ~5-15 s of training
+        e1, e2 = {"E": (0, 8), "H": (0, 4), "R": (0, 1)}[model]
         with tempfile.TemporaryDirectory() as d:
             data.write(ds, d)
-            cmd = [binary, "--datadir", d, "--outdir", d, "--size", str(dim), "--epochs", "4", "--method",
-                   str(method), "--distance", str(distance), "--rate", str(rate), "--seed", "7"]
-            stamps = _epoch_stamps(cmd, budget_s * 2)
-        if len(stamps) >= 2:
-            per_epoch = (stamps[-1] - stamps[0]) / (len(stamps) - 1)  # epoch 0 (init) excluded
-            return {"value": S / per_epoch, "unit": "triples/s", "cores": 1, "kind": "reference",
-                    "sample": f"{len(stamps) - 1} steady epochs ({S} samples each) of {os.path.basename(binary)} "
-                              f"on the same synthetic {shape}-shaped data, 1 thread (pinned to one core)"}
+            cmd = [binary, "--datadir", d, "--outdir", d, "--size", str(dim), "--method", str(method),
+                   "--distance", str(distance), "--rate", str(rate), "--seed", "7"]
+            seed_note = ""
+            if model == "R":
+                # TransR starts from TransE embeddings (transr/trainer.cpp:88-113): one
+                # reference TransE epoch, unif, writes the seed files
+                seed = os.path.join(d, "seed")
+                os.mkdir(seed)
+                subprocess.run([os.path.join(ROOT, "oracle", "_ref", "trainTransE"), "--datadir", d, "--outdir",
+                                seed, "--size", str(dim), "--method", "0", "--epochs", "1", "--seed", "7"],
+                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=budget_s * 4,
+                               check=True)
+                cmd += ["--seeddatadir", seed, "--seedmethod", "0"]
+                seed_note = ", seeded by one reference TransE epoch"
+            per_epoch = _ref_epoch_seconds(cmd, e1, e2, budget_s * 4)
+        return {"value": S / per_epoch, "unit": "triples/s", "cores": 1, "kind": "reference",
+                "sample": f"{os.path.basename(binary)} (compiled from the reference sources) on the same synthetic "
+                          f"{shape}-shaped data{seed_note}, 1 thread pinned to one core; per-epoch time = (wall of "
+                          f"{e2} epochs - wall of {e1}) / {e2 - e1}, {S} samples per epoch"}
     from oracle import orc  # CPU restatement (port) fallback
     m = orc.Model(model, dim, ds.num_entities, ds.num_relations, rate=rate, method=method, distance=distance,
                   batches=100)
@@ -193,7 +183,14 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     loss, active = eng.take_stats()
-    fold_ms, fold_n = eng.profile_query("fold" if model == "E" else "relowner")
+    # phase B: TransE runs the per-row fold and the long-row fold concurrently
+    # (timed together as "fold_phase"); TransH/TransR run the relation owners.
+    fold_ms, fold_n = eng.profile_query("fold_phase" if model == "E" else "relowner")
+    kernels_us = {}
+    for k in (("score", "fold", "fold_long") if model == "E" else ("score", "tickets", "desc", "relowner")):
+        ms, n = eng.profile_query(k)
+        if n:
+            kernels_us[k] = ms / n * 1e3
     score_ms, score_n = eng.profile_query("score")
     samples = args.steps * B
     if dist is not None:
@@ -214,7 +211,7 @@ def main():
     a = active / max(1.0, samples)
     s = 8 if args.precision == 64 else 4
     per_sample, score_bytes, fold_bytes = algorithmic_bytes_per_sample(model, dim, s, a)
-    dominant = ("fold" if model == "E" else "relowner") if fold_ms >= score_ms else "score"
+    dominant = ("fold_phase" if model == "E" else "relowner") if fold_ms >= score_ms else "score"
     if dominant == "score":
         avg_ms, bytes_per_launch = score_ms / max(1, score_n), score_bytes * B
     else:
@@ -224,7 +221,10 @@ def main():
     pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}_f{args.precision}.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get(dominant, {}).get("hbm_bytes_per_launch")
+            fams = json.load(open(pmc))
+            parts = ("fold", "fold_long") if dominant == "fold_phase" else (dominant,)
+            vals = [fams.get(p, {}).get("hbm_bytes_per_launch") for p in parts]
+            traffic = sum(v for v in vals if v) if any(vals) else None
         except (OSError, ValueError):
             traffic = None
     out = {
@@ -246,6 +246,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": dominant,
                      "kernel_avg_us": avg_ms * 1e3, "algorithmic_bytes_per_launch": bytes_per_launch,
+                     "kernels_avg_us": kernels_us,
                      "step_achieved_GBs": per_sample * samples / elapsed / 1e9},
         "active_fraction": a,
     }

@@ -207,6 +207,20 @@ struct kb2e_ctx {
     void timed(const char* name, F&& f) {
         timed_on(stream, name, f);
     }
+    // A span of work on the engine stream (e.g. several concurrent kernels
+    // joined back into it), timed from begin_span() to end_span().
+    hipEvent_t begin_span() {
+        if (!prof) return nullptr;
+        hipEvent_t a = get_event();
+        HIPCHK(hipEventRecord(a, stream));
+        return a;
+    }
+    void end_span(const char* name, hipEvent_t a) {
+        if (!a) return;
+        hipEvent_t b = get_event();
+        HIPCHK(hipEventRecord(b, stream));
+        pending.push_back({name, a, b});
+    }
     // ... or on another stream that the engine stream later waits for.
     template <class F>
     void timed_on(hipStream_t st, const char* name, F&& f) {
@@ -555,6 +569,7 @@ void run_batch_transe(kb2e_ctx* c, int64_t b) {
     // Enough waves for every touched row of a batch (<= 6 B segments).
     const int64_t max_seg = std::min<int64_t>(c->B * 6, (int64_t)c->cfg.num_entities + c->cfg.num_relations);
     const int fgrid = (int)std::max<int64_t>(1, std::min<int64_t>((max_seg + 3) / 4, 4096));
+    hipEvent_t span = c->begin_span();  // phase B as a whole: both fold kernels and the join
     if (use_long) {
         // long segments: one 4-wave workgroup each, on the fold stream, beside the per-row fold
         long_segments_kernel<<<1, 1024, 0, c->stream>>>(fa.seg_start, fa.batch_seg, fa.batch, c->long_min,
@@ -575,6 +590,7 @@ void run_batch_transe(kb2e_ctx* c, int64_t b) {
         HIPCHK(hipGetLastError());
     });
     if (use_long) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_fold_b, 0));
+    c->end_span("fold_phase", span);
 }
 
 template <typename K>

@@ -16,8 +16,10 @@ import os
 import sys
 from collections import defaultdict
 
-FAMILY = {"transe_fold_kernel": "fold", "transe_score_kernel": "score", "relowner": "relowner",
-          "transh_score": "score", "transr_score": "score", "ticket": "tickets"}
+FAMILY = {"transe_fold_long_kernel": "fold_long", "transe_fold_kernel": "fold", "transe_score_kernel": "score",
+          "relowner": "relowner", "transh_owner": "relowner", "transr_owner": "relowner",
+          "transh_score": "score", "transr_project": "score", "transr_compat": "score", "ticket": "tickets",
+          "relowner_desc": "desc", "relowner_compact": "desc", "transr_commit": "commit"}
 
 
 def family(name):
