@@ -502,11 +502,12 @@ __device__ __forceinline__ void wait_tickets3(const uint32_t* done, int count, c
 template <typename T, int CH>
 __device__ __forceinline__ void scale_row(RowReg<T, CH>& A, T len, bool apply, int n) {
     if (!apply) return;
+    const T inv = T(1) / len;  // a / len exactly, via the correctly rounded reciprocal (div_markstein)
 #pragma unroll
     for (int c = 0; c < CH; ++c)
 #pragma unroll
         for (int k = 0; k < kVec; ++k)
-            if (elem_valid(c, k, n)) A.v[c][k] = A.v[c][k] / len;
+            if (elem_valid(c, k, n)) A.v[c][k] = div_markstein(A.v[c][k], len, inv);
 }
 template <typename T, int CH>
 __device__ __forceinline__ void norm_rows3(RowReg<T, CH>& A, RowReg<T, CH>& B, RowReg<T, CH>& Wn, int n) {
@@ -696,8 +697,9 @@ __global__ __launch_bounds__(64) void transh_owner_kernel(OwnerArgs<T> a, const 
         d1 = wave_sum(d1);
         const T lR = sqrt(sR), l0 = sqrt(s0), l1 = sqrt(s1), lW = sqrt(sW);
         const T cR = lR > T(1) ? lR : T(1), c0 = l0 > T(1) ? l0 : T(1), c1 = l1 > T(1) ? l1 : T(1);
-        const bool fast = dR / (lW * cR) <= T(0.1) && d0 / (lW * c0) <= T(0.1) &&
-                          (same || d1 / (lW * c1) <= T(0.1));
+        // x = w.row / (|w| c) <= 0.1 (decisions only: compared by multiplication)
+        const bool fast = dR <= T(0.1) * (lW * cR) && d0 <= T(0.1) * (lW * c0) &&
+                          (same || d1 <= T(0.1) * (lW * c1));
         OWNER_MARK(4);
         if (fast) {
             scale_row(R, lR, lR > T(1), n);
@@ -1192,12 +1194,23 @@ __device__ __forceinline__ T transr_norm_reg(T al, T (&w)[NM], T* Wt, T* abuf, i
         if (xx <= T(1)) break;
         OWNER_COUNT(10);
         const T tmp0 = readlane_f(y, 0);
+        // Column i's sum needs a after column i-1; its per-lane product is
+        // prepared from values known before column i-1's coefficient c:
+        //   w_{i} . a_new = P1 - c (P2 - c P1),  P1 = w_i a,  P2 = w_i w_{i-1}
+        // (w_{i-1} before its update), two FMAs after c instead of five
+        // dependent operations.  The element updates themselves are the
+        // reference's operations, off the serial path.
+        T prod = T(0);
 #pragma unroll
         for (int i = 0; i < NM; ++i) {
-            const T tmp = i == 0 ? tmp0 : wave_sum(w[i] * al);
+            const T tmp = i == 0 ? tmp0 : wave_sum(prod);
             // learningRate_ * lambda * (2 tmp), lambda = 1: the doubling is exact,
             // so (2 lr) * tmp rounds the same real number once, as the reference
             const T coef = lr2 * tmp;
+            if (i + 1 < NM) {
+                const T P1 = w[i + 1] * al, P2 = w[i + 1] * w[i];
+                prod = fma(-coef, fma(-coef, P1, P2), P1);
+            }
             w[i] = w[i] - coef * al;
             al = al - coef * w[i];
         }
