@@ -128,6 +128,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", default="transe_fb15k", choices=sorted(CONFIGS))
     ap.add_argument("--precision", type=int, default=64, choices=[32, 64])
+    ap.add_argument("--schedule", default="ordered", choices=["ordered", "parallel"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -149,7 +150,8 @@ def main():
     train = shard_heads(ds.train, rank, world) if world > 1 else ds.train
     batches = 100
     eng = Engine(model, dim, ds.num_entities, ds.num_relations, rate=rate, method=method, distance=distance,
-                 batches=batches, seed=7 + rank, precision=args.precision, device=local if world > 1 else 0)
+                 batches=batches, seed=7 + rank, precision=args.precision, device=local if world > 1 else 0,
+                 schedule=args.schedule)
     eng.upload_triples(train)
     ent, rel, w = eng.init_params()
     if model == "R":
@@ -174,7 +176,9 @@ def main():
     run(args.warmup)
     eng.synchronize()
     eng.take_stats()
-    eng.profile(True)
+    # HIP-event timing of the batch kernels on every 10th batch (events cost
+    # device time; sampling keeps the timed run unperturbed)
+    eng.profile(10)
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
@@ -188,7 +192,7 @@ def main():
     # (timed together as "fold_phase"); TransH/TransR run the relation owners.
     fold_ms, fold_n = eng.profile_query("fold_phase" if model == "E" else "relowner")
     kernels_us = {}
-    for k in (("score", "fold", "fold_long") if model == "E" else ("score", "tickets", "desc", "relowner")):
+    for k in (("score", "fold", "fold_long", "apply", "apply_long") if model == "E" else ("score", "tickets", "desc", "relowner")):
         ms, n = eng.profile_query(k)
         if n:
             kernels_us[k] = ms / n * 1e3

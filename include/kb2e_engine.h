@@ -48,6 +48,22 @@ typedef enum {
     KB2E_SAMPLER_REPLAY = 1  /* caller supplies the stream (kb2e_set_sample_stream) */
 } kb2e_sampler;
 
+/* How a batch's updates are applied to the *_next_ tables.  Both schedules
+ * score every sample and compute every update direction from the
+ * start-of-batch tables, as the reference does (common/trainer.cpp:130-149). */
+typedef enum {
+    KB2E_SCHEDULE_ORDERED = 0,  /* the reference's sequence: sample by sample, a
+                                   norm after every update (transe/trainer.cpp:38-45,
+                                   transh/trainer.cpp:48-58, transr/trainer.cpp:
+                                   166-187); results equal the reference's (default) */
+    KB2E_SCHEDULE_PARALLEL = 1  /* each touched row / relation gets its summed
+                                   delta, then the model's norms and constraints
+                                   once per batch; equal to ORDERED for rows with
+                                   one update per batch, O(lr^2) apart otherwise.
+                                   Parity is statistical (link-prediction quality,
+                                   DESIGN.md) */
+} kb2e_schedule;
+
 typedef struct {
     int32_t model;          /* kb2e_model */
     int32_t dim;            /* --size (common/args.cpp:71-74) */
@@ -64,6 +80,7 @@ typedef struct {
     int32_t transr_compat;  /* 1: reproduce the accumulating TransR energy of
                                transr/transr.cpp:20-25; 0: zeroed work vectors */
     int32_t device;         /* HIP device ordinal */
+    int32_t schedule;       /* kb2e_schedule */
 } kb2e_config;
 
 typedef struct kb2e_ctx kb2e_ctx;
@@ -146,8 +163,11 @@ int32_t kb2e_rng_next(kb2e_ctx* ctx);
 
 /* Timing of the engine's device kernels on the engine's own HIP stream (HIP
  * events around each launch; off by default).  `name` is a kernel family
- * ("score", "fold", "index", "sample", ...).  Returns total milliseconds and
- * launch count since kb2e_profile_enable(ctx, 1). */
+ * ("score", "fold", "apply", "relowner", "index", "sample", ...).  Returns total
+ * milliseconds and launch count since kb2e_profile_enable.  on = 0: off;
+ * on = P >= 1: the batch kernels of every P-th batch are timed (event records
+ * cost device time of their own; sampling keeps the rest of the run unperturbed),
+ * per-epoch kernels always. */
 kb2e_status kb2e_profile_enable(kb2e_ctx* ctx, int32_t on);
 kb2e_status kb2e_profile_query(kb2e_ctx* ctx, const char* name, double* total_ms, int64_t* launches);
 

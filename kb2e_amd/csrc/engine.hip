@@ -33,6 +33,8 @@
 #include "kernels_relowner.hpp"
 #include "kernels_sampler.hpp"
 #include "kernels_eval.hpp"
+#include "kernels_parallel.hpp"
+#include "kernels_transr_parallel.hpp"
 
 using namespace kb2e;
 
@@ -49,6 +51,8 @@ struct HipError : std::runtime_error {
             throw HipError(std::string(#expr) + ": " + hipGetErrorString(_e) + " @" +             \
                            std::to_string(__LINE__));                                             \
     } while (0)
+
+constexpr int kGlibcBlock = 4096;  // words per block of the device glibc generator
 
 int bits_for(int64_t v) {  // bits to hold values 0..v
     int b = 1;
@@ -90,6 +94,10 @@ void run_batch_relowner(kb2e_ctx* c, int64_t b);
 void check_dataflow(kb2e_ctx* c);
 void build_owner_index(kb2e_ctx* c);
 void prepare_relowner_kernels();
+void setup_transr_parallel(kb2e_ctx* c);
+void build_transr_tiles(kb2e_ctx* c);
+template <typename T>
+void run_batch_transr_parallel(kb2e_ctx* c, int64_t b);
 }  // namespace
 
 struct kb2e_ctx {
@@ -119,9 +127,9 @@ struct kb2e_ctx {
     // made on the host, the rejection chain is resolved on the device.
     hipStream_t side_stream = nullptr;
     DevBuf words, levels, jfin, sidefin, filter_slots, pr_dev, consumed_dev;
-    int32_t* pin_words = nullptr;
     int64_t* pin_consumed = nullptr;
-    std::vector<uint32_t> raw_vals;
+    uint32_t* pin_win = nullptr;            // generator window after the epoch (31 words)
+    DevBuf raw_words, glibc_starts, glibc_table, win_dev;
     int64_t nraw = 0, nraw_cap = 0;
     double words_per_sample = 6.0;
     bool prefetch_valid = false;   // set cur^1 holds the stream for the current rng state
@@ -148,6 +156,16 @@ struct kb2e_ctx {
     uint32_t batch_stamp = 0;
     int32_t gram_min = 48;  // KB2E_GRAM_MIN: fold segments this long use the scalar recurrence (0 = off)
     int32_t long_min = 192;  // KB2E_FOLD_LONG: segments this long take the 4-wave fold (0 = off; L1 only)
+    int32_t apply_long_min = 256;  // KB2E_APPLY_LONG: PARALLEL-schedule segments this long take a 16-wave workgroup
+    int32_t par_long_cap = 1, apply_grid = 256;
+    DevBuf par_long_list, par_long_count;  // per epoch: long segments of every batch
+    // PARALLEL schedule: per-event records in sorted order (kernels_transe.hpp EventRecs)
+    DevBuf ev_iota, ev_slot_sorted, ev_inv, seg_row, ev_meta, ev_words;
+    // PARALLEL TransR (kernels_transr_parallel.hpp)
+    int32_t rpar_St = 8, rpar_max_tiles = 1;
+    bool rpar_no_constraint = false;
+    DevBuf rpar_y, rpar_wpart, rpar_rpart, rpar_tile_act, rpar_pair, rpar_relpair, rpar_relpair_stamp, rpar_tiles,
+        rpar_ntiles, rpar_tile_first, rpar_rel_begin;
     hipStream_t fold_stream = nullptr;  // the long-segment fold runs beside the per-row fold
     hipEvent_t ev_fold_a = nullptr, ev_fold_b = nullptr;
     DevBuf long_list, long_count;
@@ -161,6 +179,9 @@ struct kb2e_ctx {
     bool epoch_ready = false;
     // profiling
     bool prof = false;
+    int32_t prof_period = 1;   // time the batch kernels of every prof_period-th batch
+    int64_t prof_counter = 0;
+    bool prof_batch = true;    // the batch being queued is timed
     std::map<std::string, Timer> timers;
     struct Pending {
         std::string name;
@@ -173,7 +194,7 @@ struct kb2e_ctx {
         if (pin_si) (void)hipHostFree(pin_si);
         if (pin_sj) (void)hipHostFree(pin_sj);
         if (pin_side) (void)hipHostFree(pin_side);
-        if (pin_words) (void)hipHostFree(pin_words);
+        if (pin_win) (void)hipHostFree(pin_win);
         if (pin_consumed) (void)hipHostFree(pin_consumed);
         flush_timers();
         if (ev_sampled) (void)hipEventDestroy(ev_sampled);
@@ -187,6 +208,7 @@ struct kb2e_ctx {
     }
 
     bool f64() const { return cfg.precision == 64; }
+    bool parallel() const { return cfg.schedule == KB2E_SCHEDULE_PARALLEL; }
     int32_t* si() const { return si_[cur].as<int32_t>(); }
     int32_t* sj() const { return sj_[cur].as<int32_t>(); }
     uint8_t* side() const { return side_[cur].as<uint8_t>(); }
@@ -210,7 +232,7 @@ struct kb2e_ctx {
     // A span of work on the engine stream (e.g. several concurrent kernels
     // joined back into it), timed from begin_span() to end_span().
     hipEvent_t begin_span() {
-        if (!prof) return nullptr;
+        if (!prof || !prof_batch) return nullptr;
         hipEvent_t a = get_event();
         HIPCHK(hipEventRecord(a, stream));
         return a;
@@ -224,7 +246,7 @@ struct kb2e_ctx {
     // ... or on another stream that the engine stream later waits for.
     template <class F>
     void timed_on(hipStream_t st, const char* name, F&& f) {
-        if (!prof) {
+        if (!prof || !prof_batch) {
             f();
             return;
         }
@@ -346,9 +368,19 @@ void build_index(kb2e_ctx* c) {
             emit_keys_kernel<6, false><<<grid, 256, 0, c->stream>>>(ka);
         HIPCHK(hipGetLastError());
         size_t tb = c->sort_tmp_bytes;
-        HIPCHK(hipcub::DeviceRadixSort::SortKeys(c->sort_tmp.p, tb, c->keys.as<uint64_t>(),
-                                                 c->keys_sorted.as<uint64_t>(), (int)nkeys, 0,
-                                                 c->kl.total_bits(), c->stream));
+        if (c->parallel()) {  // the sorted position of every emitted key, for phase A's event records
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tb, c->keys.as<uint64_t>(),
+                                                      c->keys_sorted.as<uint64_t>(), c->ev_iota.as<int32_t>(),
+                                                      c->ev_slot_sorted.as<int32_t>(), (int)nkeys, 0,
+                                                      c->kl.total_bits(), c->stream));
+            inverse_perm_kernel<<<(int)((nkeys + 255) / 256), 256, 0, c->stream>>>(c->ev_slot_sorted.as<int32_t>(),
+                                                                                  nkeys, c->ev_inv.as<int32_t>());
+            HIPCHK(hipGetLastError());
+        } else {
+            HIPCHK(hipcub::DeviceRadixSort::SortKeys(c->sort_tmp.p, tb, c->keys.as<uint64_t>(),
+                                                     c->keys_sorted.as<uint64_t>(), (int)nkeys, 0,
+                                                     c->kl.total_bits(), c->stream));
+        }
         const int g2 = (int)((nkeys + 255) / 256);
         seg_flags_kernel<<<g2, 256, 0, c->stream>>>(c->keys_sorted.as<uint64_t>(), nkeys, c->kl,
                                                      c->flags.as<int32_t>(), c->nvalid.as<int32_t>());
@@ -364,7 +396,19 @@ void build_index(kb2e_ctx* c) {
                                                         c->nseg.as<int32_t>(), (int)c->nb, c->kl,
                                                         c->batch_seg.as<int32_t>());
         HIPCHK(hipGetLastError());
-        if (c->cfg.model != KB2E_TRANSE) build_owner_index(c);
+        if (c->cfg.model != KB2E_TRANSE && !c->parallel()) build_owner_index(c);
+        if (c->parallel()) {
+            seg_rows_kernel<<<256, 256, 0, c->stream>>>(c->keys_sorted.as<uint64_t>(), c->seg_start.as<int32_t>(),
+                                                       c->nseg.as<int32_t>(), c->kl, c->seg_row.as<int32_t>());
+            HIPCHK(hipGetLastError());
+            if (c->cfg.model == KB2E_TRANSR) build_transr_tiles(c);
+        }
+        if (c->cfg.model == KB2E_TRANSE && c->cfg.schedule == KB2E_SCHEDULE_PARALLEL && c->apply_long_min > 0) {
+            long_lists_kernel<<<(int)c->nb, 1024, 0, c->stream>>>(
+                c->seg_start.as<int32_t>(), c->batch_seg.as<int32_t>(), c->apply_long_min, c->par_long_cap,
+                c->par_long_list.as<int32_t>(), c->par_long_count.as<int32_t>());
+            HIPCHK(hipGetLastError());
+        }
     });
 }
 
@@ -383,31 +427,41 @@ void ensure_sampler_capacity(kb2e_ctx* c, int64_t nraw) {
     c->levels.alloc((size_t)K * (nraw + 1) * 4);
     c->jfin.alloc(nraw * 4);
     c->sidefin.alloc(nraw);
-    if (c->pin_words) (void)hipHostFree(c->pin_words);
-    HIPCHK(hipHostMalloc((void**)&c->pin_words, nraw * 4, 0));
-    c->raw_vals.resize(nraw);
+    c->raw_words.alloc((nraw + GlibcRand::kDeg) * 4);
+    c->glibc_starts.alloc(((nraw + kGlibcBlock - 1) / kGlibcBlock) * GlibcRand::kDeg * 4);
     c->nraw_cap = nraw;
 }
 
 // Draw the stream of the epoch that follows the committed rng state into set
-// cur^1, on the side stream: host makes the raw glibc words, the device
-// resolves the rejection chain (kernels_sampler.hpp).  Nothing is committed
-// until start_epoch consumes it.
+// cur^1, on the side stream: the device makes the epoch's raw glibc words from
+// the generator's 31-word window (jump table, kernels_sampler.hpp) and resolves
+// the rejection chain.  Nothing is committed until start_epoch consumes it.
 void launch_prefetch(kb2e_ctx* c) {
     const int set = c->cur ^ 1;
     const int64_t nraw = (int64_t)(c->words_per_sample * c->S) + 4096;
     ensure_sampler_capacity(c, nraw);
     c->nraw = nraw;
-    GlibcRand g = c->rng;
-    for (int64_t q = 0; q < nraw; ++q) {
-        const uint32_t v = g.next_raw();
-        c->raw_vals[q] = v;
-        c->pin_words[q] = (int32_t)(v >> 1);
+    if (!c->glibc_table.p) {
+        std::vector<uint32_t> C((size_t)GlibcRand::kDeg * kGlibcBlock);
+        glibc_jump_table(kGlibcBlock, C.data());
+        c->glibc_table.alloc(C.size() * 4);
+        HIPCHK(hipMemcpy(c->glibc_table.p, C.data(), C.size() * 4, hipMemcpyHostToDevice));
     }
+    GlibcWindow win;
+    c->rng.window(win.w);
     hipStream_t st = c->side_stream;
     // set cur^1 may still be read by the epoch before the current one
     HIPCHK(hipStreamWaitEvent(st, c->ev_epoch_done, 0));
-    HIPCHK(hipMemcpyAsync(c->words.p, c->pin_words, nraw * 4, hipMemcpyHostToDevice, st));
+    {
+        const int64_t nblocks = (nraw + kGlibcBlock - 1) / kGlibcBlock;
+        glibc_starts_kernel<<<1, 64, 0, st>>>(win, c->glibc_table.as<uint32_t>(), kGlibcBlock, (int32_t)nblocks,
+                                              c->glibc_starts.as<uint32_t>(), c->raw_words.as<uint32_t>());
+        HIPCHK(hipGetLastError());
+        glibc_words_kernel<<<(int)((nraw + 255) / 256), 256, 0, st>>>(
+            c->glibc_table.as<uint32_t>(), kGlibcBlock, c->glibc_starts.as<uint32_t>(), nraw,
+            c->raw_words.as<uint32_t>(), c->words.as<int32_t>());
+        HIPCHK(hipGetLastError());
+    }
     const int K = std::max(1, bits_for(std::max<int64_t>(c->S - 1, 1)));
     SamplerArgs a{};
     a.words = c->words.as<int32_t>();
@@ -462,7 +516,11 @@ void launch_prefetch(kb2e_ctx* c) {
     } else {
         launch();
     }
+    glibc_window_kernel<<<1, 64, 0, st>>>(c->raw_words.as<uint32_t>(), c->consumed_dev.as<int64_t>(),
+                                          c->win_dev.as<uint32_t>());
+    HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->pin_consumed, c->consumed_dev.p, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->pin_win, c->win_dev.p, GlibcRand::kDeg * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(c->ev_sampled, st));
     c->prefetch_valid = true;
     c->prefetch_version = c->rng_version;
@@ -495,7 +553,7 @@ void start_epoch_stream(kb2e_ctx* c) {
         HIPCHK(hipEventSynchronize(c->ev_sampled));
         const int64_t used = *c->pin_consumed;
         if (used >= 0) {
-            c->rng.commit(c->raw_vals.data(), used);
+            c->rng.set_window(c->pin_win);  // the generator after the epoch's `used` words
             c->rng_version++;
             c->words_per_sample = std::max(c->words_per_sample, 1.02 * (double)used / (double)c->S);
             break;
@@ -509,6 +567,10 @@ void start_epoch_stream(kb2e_ctx* c) {
     c->prefetch_valid = false;
     c->cur ^= 1;
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_sampled, 0));
+    // Draw the next epoch's stream now, beside this epoch's batches: it writes
+    // the set the previous epoch read (the side stream waits for that epoch's
+    // end marker) and its rng start is this epoch's committed end.
+    launch_prefetch(c);
 }
 
 // --------------------------------------------------------------- the batch
@@ -526,6 +588,7 @@ ScoreArgs<T> score_args(kb2e_ctx* c, int64_t b) {
     a.n = c->n;
     a.ld = c->ld;
     a.nw = c->nw;
+    a.ne = c->cfg.num_entities;
     a.ent = c->ent.as<T>();
     a.rel = c->rel.as<T>();
     a.w = c->w.as<T>();
@@ -593,6 +656,62 @@ void run_batch_transe(kb2e_ctx* c, int64_t b) {
     c->end_span("fold_phase", span);
 }
 
+EventRecs event_recs(kb2e_ctx* c) {
+    EventRecs er{};
+    er.meta = c->ev_meta.as<int32_t>();
+    er.words = c->ev_words.as<uint64_t>();
+    er.inv = c->ev_inv.as<int32_t>();
+    er.keys = c->keys.as<uint64_t>();
+    er.seg_row = c->seg_row.as<int32_t>();
+    er.slots = c->slots;
+    return er;
+}
+
+// PARALLEL schedule (kernels_parallel.hpp): the same phase A, then every
+// touched row gets its summed delta and one norm.  Long segments (the hot
+// relations and entities) take a 16-wave workgroup each.
+template <typename T, int CH>
+void run_batch_transe_parallel(kb2e_ctx* c, int64_t b) {
+    ScoreArgs<T> sa = score_args<T>(c, b);
+    const bool l1 = c->cfg.distance == 0;
+    const int grid = (int)((c->B + 3) / 4);
+    const EventRecs er = event_recs(c);
+    c->timed("score", [&] {
+        if (l1) transe_score_kernel<T, CH, true, true><<<grid, 256, 0, c->stream>>>(sa, er, c->kl, b * c->B);
+        else transe_score_kernel<T, CH, false, true><<<grid, 256, 0, c->stream>>>(sa, er, c->kl, b * c->B);
+        HIPCHK(hipGetLastError());
+    });
+    FoldArgs<T> fa{};
+    fa.keys = c->keys_sorted.as<uint64_t>();
+    fa.seg_start = c->seg_start.as<int32_t>();
+    fa.batch_seg = c->batch_seg.as<int32_t>();
+    fa.batch = (int32_t)b;
+    fa.kl = c->kl;
+    fa.ne = c->cfg.num_entities;
+    fa.n = c->n;
+    fa.ld = c->ld;
+    fa.nw = c->nw;
+    fa.ent = c->ent.as<T>();
+    fa.rel = c->rel.as<T>();
+    fa.lr = c->cfg.learning_rate;
+    fa.act = sa.act;
+    fa.xbits = sa.xbits;
+    fa.xreal = sa.xreal;
+    fa.gram_min = 0;
+    fa.long_min = c->apply_long_min;
+    hipEvent_t span = c->begin_span();
+    c->timed("apply", [&] {
+        if (l1)
+            transe_apply_kernel<T, CH, true><<<c->apply_grid, 1024, 0, c->stream>>>(
+                fa, er, c->par_long_list.as<int32_t>(), c->par_long_count.as<int32_t>(), c->par_long_cap);
+        else
+            transe_apply_kernel<T, CH, false><<<c->apply_grid, 1024, 0, c->stream>>>(
+                fa, er, c->par_long_list.as<int32_t>(), c->par_long_count.as<int32_t>(), c->par_long_cap);
+        HIPCHK(hipGetLastError());
+    });
+    c->end_span("fold_phase", span);
+}
+
 template <typename K>
 void allow_lds(K kernel, size_t bytes) {
     (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
@@ -609,22 +728,37 @@ void prepare_fold_long_kernels() {
 
 template <typename T>
 void run_batch(kb2e_ctx* c, int64_t b) {
-    if (c->cfg.model == KB2E_TRANSE) {
+    if (c->cfg.model == KB2E_TRANSE && c->cfg.schedule == KB2E_SCHEDULE_PARALLEL) {
+        switch (c->ch) {
+            case 1: run_batch_transe_parallel<T, 1>(c, b); break;
+            case 2: run_batch_transe_parallel<T, 2>(c, b); break;
+            default: run_batch_transe_parallel<T, 4>(c, b); break;
+        }
+    } else if (c->cfg.model == KB2E_TRANSE) {
         switch (c->ch) {
             case 1: run_batch_transe<T, 1>(c, b); break;
             case 2: run_batch_transe<T, 2>(c, b); break;
             default: run_batch_transe<T, 4>(c, b); break;
         }
+    } else if (c->cfg.model == KB2E_TRANSR && c->parallel()) {
+        run_batch_transr_parallel<T>(c, b);
     } else {
         run_batch_relowner<T>(c, b);
     }
 }
 
-__global__ void reduce_stats_kernel(const double* loss, const uint8_t* act, int64_t lo, int64_t hi, double* out) {
-    __shared__ double sl[1024];
-    __shared__ double sa[1024];
+// Epoch statistics (loss, hinge-active count) summed on the device without a
+// host round trip: 256 fixed slices summed by one block each, then the slices
+// in order by one block into the running accumulator.  Deterministic.
+constexpr int kStatSlices = 256;
+
+__global__ __launch_bounds__(256) void stats_partial_kernel(const double* loss, const uint8_t* act, int64_t lo,
+                                                            int64_t hi, double* part) {
+    __shared__ double sl[256], sa[256];
+    const int64_t n = hi - lo;
+    const int64_t b0 = lo + n * blockIdx.x / kStatSlices, b1 = lo + n * (blockIdx.x + 1) / kStatSlices;
     double l = 0, a = 0;
-    for (int64_t k = lo + threadIdx.x; k < hi; k += blockDim.x) {
+    for (int64_t k = b0 + threadIdx.x; k < b1; k += blockDim.x) {
         l += loss[k];
         a += act[k];
     }
@@ -639,24 +773,50 @@ __global__ void reduce_stats_kernel(const double* loss, const uint8_t* act, int6
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        out[0] = sl[0];
-        out[1] = sa[0];
+        part[2 * blockIdx.x] = sl[0];
+        part[2 * blockIdx.x + 1] = sa[0];
     }
 }
 
-// Fold the stats of samples [reduced_upto, upto) of the current epoch into the
-// host accumulators (synchronises the stream).
+__global__ __launch_bounds__(256) void stats_final_kernel(const double* part, double* acc) {
+    __shared__ double sl[kStatSlices], sa[kStatSlices];
+    sl[threadIdx.x] = part[2 * threadIdx.x];
+    sa[threadIdx.x] = part[2 * threadIdx.x + 1];
+    __syncthreads();
+    for (int s = kStatSlices / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            sl[threadIdx.x] += sl[threadIdx.x + s];
+            sa[threadIdx.x] += sa[threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        acc[0] += sl[0];
+        acc[1] += sa[0];
+    }
+}
+
+// Queue the sums of samples [reduced_upto, upto) of the current epoch into the
+// device accumulator (asynchronous).
 void reduce_stats(kb2e_ctx* c, int64_t upto) {
     if (upto <= c->reduced_upto) return;
-    reduce_stats_kernel<<<1, 1024, 0, c->stream>>>(c->loss.as<double>(), c->act.as<uint8_t>(), c->reduced_upto,
-                                                   upto, c->stats.as<double>());
+    double* part = c->stats.as<double>() + 2;
+    stats_partial_kernel<<<kStatSlices, 256, 0, c->stream>>>(c->loss.as<double>(), c->act.as<uint8_t>(),
+                                                               c->reduced_upto, upto, part);
     HIPCHK(hipGetLastError());
+    stats_final_kernel<<<1, kStatSlices, 0, c->stream>>>(part, c->stats.as<double>());
+    HIPCHK(hipGetLastError());
+    c->reduced_upto = upto;
+}
+
+// Move the device accumulator into the host totals (synchronises the stream).
+void collect_stats(kb2e_ctx* c) {
     double h[2];
     HIPCHK(hipMemcpyAsync(h, c->stats.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemsetAsync(c->stats.p, 0, sizeof(h), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->acc_loss += h[0];
     c->acc_active += (int64_t)llround(h[1]);
-    c->reduced_upto = upto;
     check_dataflow(c);
 }
 
@@ -669,13 +829,14 @@ void run_batches(kb2e_ctx* c, int64_t count) {
             c->epoch_ready = true;
             c->reduced_upto = 0;
         }
+        c->prof_batch = (c->prof_counter++ % c->prof_period) == 0;
         if (c->f64()) run_batch<double>(c, c->epoch_pos);
         else run_batch<float>(c, c->epoch_pos);
+        c->prof_batch = true;
         if (++c->epoch_pos == c->nb) {
             // Overlap the next epoch's sampling with this epoch's batches.  It
             // writes the set the previous epoch read, so it waits for the
             // previous epoch's end marker (recorded below for the next one).
-            if (c->cfg.sampler == KB2E_SAMPLER_GLIBC && !c->host_sampler) launch_prefetch(c);
             HIPCHK(hipEventRecord(c->ev_epoch_done, c->stream));
             reduce_stats(c, c->S);
             c->epoch_pos = 0;
@@ -725,6 +886,8 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     c->nraw_cap = 0;
     c->consumed_dev.alloc(16);
     if (!c->pin_consumed) HIPCHK(hipHostMalloc((void**)&c->pin_consumed, 16, 0));
+    if (!c->pin_win) HIPCHK(hipHostMalloc((void**)&c->pin_win, 32 * 4, 0));
+    c->win_dev.alloc(32 * 4);
     if (c->pin_si) { (void)hipHostFree(c->pin_si); (void)hipHostFree(c->pin_sj); (void)hipHostFree(c->pin_side); }
     HIPCHK(hipHostMalloc((void**)&c->pin_si, c->S * 4, 0));
     HIPCHK(hipHostMalloc((void**)&c->pin_sj, c->S * 4, 0));
@@ -746,20 +909,46 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     c->nseg.alloc(16);
     c->nvalid.alloc(16);
     c->batch_seg.alloc((c->nb + 1) * 4);
-    size_t t1 = 0, t2 = 0;
+    size_t t1 = 0, t2 = 0, t3 = 0;
     HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, t1, (uint64_t*)nullptr, (uint64_t*)nullptr, (int)nkeys, 0,
                                              c->kl.total_bits(), c->stream));
+    if (c->parallel()) {
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, t3, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                  (int32_t*)nullptr, (int32_t*)nullptr, (int)nkeys, 0,
+                                                  c->kl.total_bits(), c->stream));
+        c->ev_iota.alloc(nkeys * 4);
+        std::vector<int32_t> iota((size_t)nkeys);
+        for (int64_t q = 0; q < nkeys; ++q) iota[q] = (int32_t)q;
+        HIPCHK(hipMemcpy(c->ev_iota.p, iota.data(), nkeys * 4, hipMemcpyHostToDevice));
+        c->ev_slot_sorted.alloc(nkeys * 4);
+        c->ev_inv.alloc(nkeys * 4);
+        c->seg_row.alloc((nkeys + 1) * 4);
+        c->ev_meta.alloc(nkeys * 4);
+        c->ev_words.alloc((size_t)nkeys * c->nw * 8);
+    }
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (int32_t*)nullptr, (int32_t*)nullptr, (int)nkeys,
                                             c->stream));
-    c->sort_tmp_bytes = std::max(t1, t2);
+    c->sort_tmp_bytes = std::max(std::max(t1, t2), t3);
     c->sort_tmp.alloc(c->sort_tmp_bytes);
     c->act.alloc(c->S);
     c->loss.alloc(c->S * 8);
     c->xbits.alloc((size_t)c->B * 2 * c->nw * 8);
     if (g.distance != 0 || g.model == KB2E_TRANSR)
         c->xreal.alloc((size_t)c->B * 2 * c->ld * c->esize);
-    c->stats.alloc(64);
+    c->stats.alloc((2 + 2 * kStatSlices) * 8);
+    HIPCHK(hipMemset(c->stats.p, 0, c->stats.bytes));
+    if (g.model == KB2E_TRANSE && g.schedule == KB2E_SCHEDULE_PARALLEL) {
+        const int64_t per_batch = c->B * c->slots;
+        c->par_long_cap = (int32_t)(c->apply_long_min > 0 ? std::min<int64_t>(per_batch, per_batch / c->apply_long_min + 1)
+                                                         : 1);
+        c->par_long_list.alloc((size_t)c->nb * c->par_long_cap * 4);
+        c->par_long_count.alloc((size_t)c->nb * 4);
+        // one 16-wave workgroup per CU, and at least one per long segment
+        c->apply_grid = std::max(2 * c->num_cus, std::min<int>(c->par_long_cap, 4096));
+        if (const char* ag = getenv("KB2E_APPLY_GRID")) c->apply_grid = std::max(1, atoi(ag));
+    }
     setup_relowner_buffers(c);
+    if (g.model == KB2E_TRANSR && g.schedule == KB2E_SCHEDULE_PARALLEL) setup_transr_parallel(c);
     c->device_bytes = 0;
     for (DevBuf* d : {&c->ent, &c->rel, &c->w, &c->heads, &c->tails, &c->rels, &c->si_[0], &c->sj_[0], &c->side_[0],
                       &c->si_[1], &c->sj_[1], &c->side_[1], &c->filter_slots, &c->pr_dev,
@@ -771,6 +960,7 @@ void setup_epoch_buffers(kb2e_ctx* c) {
 }  // namespace
 
 #include "engine_relowner.inc"
+#include "engine_transr_parallel.inc"
 
 namespace {
 template <typename T, int CH>
@@ -807,6 +997,7 @@ void kb2e_default_config(kb2e_config* cfg) {
     cfg->sampler = KB2E_SAMPLER_GLIBC;
     cfg->transr_compat = 1;
     cfg->device = 0;
+    cfg->schedule = KB2E_SCHEDULE_ORDERED;
 }
 
 kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
@@ -815,9 +1006,12 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
     const kb2e_config& g = *cfg;
     if (g.model < 0 || g.model > 2 || g.dim < 1 || g.dim > 512 || g.num_entities < 1 || g.num_relations < 1 ||
         g.num_batches < 1 || (g.precision != 32 && g.precision != 64) || (g.method != 0 && g.method != 1) ||
-        (g.distance != 0 && g.distance != 1) || (g.sampler != 0 && g.sampler != 1))
+        (g.distance != 0 && g.distance != 1) || (g.sampler != 0 && g.sampler != 1) ||
+        (g.schedule != KB2E_SCHEDULE_ORDERED && g.schedule != KB2E_SCHEDULE_PARALLEL))
         return KB2E_EINVAL;
-    if (g.model == KB2E_TRANSR && g.num_relations > g.num_entities) return KB2E_EINVAL;  // entityVec_next_[relation]
+    if (g.model == KB2E_TRANSR && g.num_relations > g.num_entities) return KB2E_EINVAL;
+    if (g.schedule == KB2E_SCHEDULE_PARALLEL && g.model == KB2E_TRANSH) return KB2E_EUNSUPPORTED;
+    if (g.schedule == KB2E_SCHEDULE_PARALLEL && g.model == KB2E_TRANSR && g.dim > 128) return KB2E_EUNSUPPORTED;  // entityVec_next_[relation]
     if (g.model == KB2E_TRANSR && ((size_t)g.dim * (g.dim + 1) + 3 * (size_t)g.dim) * (g.precision / 8) > 96 * 1024)
         return KB2E_EUNSUPPORTED;  // the owner's relation matrix must fit in LDS
     std::unique_ptr<kb2e_ctx> c(new kb2e_ctx());
@@ -841,6 +1035,7 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
         prepare_fold_long_kernels();
         if (const char* gm = getenv("KB2E_GRAM_MIN")) c->gram_min = atoi(gm);
         if (const char* lm = getenv("KB2E_FOLD_LONG")) c->long_min = atoi(lm);
+        if (const char* al = getenv("KB2E_APPLY_LONG")) c->apply_long_min = atoi(al);
         const char* hs = getenv("KB2E_HOST_SAMPLER");
         c->host_sampler = hs && hs[0] == '1';
         setup_buffers(c.get());
@@ -878,7 +1073,14 @@ kb2e_status kb2e_upload_triples(kb2e_ctx* c, const int32_t* h, const int32_t* t,
         if (c->cfg.method == 0) std::fill(pr.begin(), pr.end(), 500.0);  // common/trainer.cpp:84-86
         c->pr_dev.alloc(pr.size() * 8);
         HIPCHK(hipMemcpy(c->pr_dev.p, pr.data(), pr.size() * 8, hipMemcpyHostToDevice));
-        if (c->cfg.model != KB2E_TRANSE) plan_owners(c->plan, c->ts, c->cfg.num_relations, c->num_cus);
+        if (c->cfg.model == KB2E_TRANSR && c->parallel()) {
+            // PARALLEL TransR: every relation is its own event row (relation segments = tiles)
+            c->plan.num_owners = c->cfg.num_relations;
+            c->plan.owner.resize(c->cfg.num_relations);
+            for (int r = 0; r < c->cfg.num_relations; ++r) c->plan.owner[r] = r;
+        } else if (c->cfg.model != KB2E_TRANSE) {
+            plan_owners(c->plan, c->ts, c->cfg.num_relations, c->num_cus);
+        }
         setup_epoch_buffers(c);
         // setup used the legacy stream (hipMemset/hipMemcpy): the non-blocking
         // engine stream does not order against it, so drain it here
@@ -1056,7 +1258,10 @@ kb2e_status kb2e_synchronize(kb2e_ctx* c) {
 
 kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
     return guarded(c, [&] {
-        if (c->have_triples) reduce_stats(c, c->epoch_pos * c->B);
+        if (c->have_triples) {
+            reduce_stats(c, c->epoch_pos * c->B);
+            collect_stats(c);
+        }
 #ifdef KB2E_OWNER_PROF
         {
             std::vector<unsigned long long> pr((size_t)kProfOwners * 16);
@@ -1100,8 +1305,9 @@ kb2e_status kb2e_train_epoch(kb2e_ctx* c, double* loss, int64_t* active) {
         HIPCHK(hipSetDevice(c->cfg.device));
         c->acc_loss = 0;
         c->acc_active = 0;
+        HIPCHK(hipMemsetAsync(c->stats.p, 0, 16, c->stream));  // only this epoch's statistics
         run_batches(c, c->nb);
-        HIPCHK(hipStreamSynchronize(c->stream));
+        collect_stats(c);
         if (loss) *loss = c->acc_loss;
         if (active) *active = c->acc_active;
         c->acc_loss = 0;
@@ -1163,13 +1369,13 @@ kb2e_status kb2e_evaluate(kb2e_ctx* c, const int32_t* th, const int32_t* tt, con
                 if (c->f64()) {
                     EvalArgs<double> ea{c->cfg.model, n, c->ld, ne, c->cfg.distance == 0 || c->cfg.model == KB2E_TRANSH,
                                         c->ent.as<double>(), c->rel.as<double>(),
-                                        c->cfg.model == KB2E_TRANSR ? c->wsnap.as<double>() : c->w.as<double>(), r,
+                                        c->cfg.model == KB2E_TRANSR && !c->parallel() ? c->wsnap.as<double>() : c->w.as<double>(), r,
                                         d_PT.as<double>(), d_relv.as<double>()};
                     eval_project_kernel<double><<<pg, 256, 0, c->stream>>>(ea);
                 } else {
                     EvalArgs<float> ea{c->cfg.model, n, c->ld, ne, c->cfg.distance == 0 || c->cfg.model == KB2E_TRANSH,
                                        c->ent.as<float>(), c->rel.as<float>(),
-                                       c->cfg.model == KB2E_TRANSR ? c->wsnap.as<float>() : c->w.as<float>(), r,
+                                       c->cfg.model == KB2E_TRANSR && !c->parallel() ? c->wsnap.as<float>() : c->w.as<float>(), r,
                                        d_PT.as<double>(), d_relv.as<double>()};
                     eval_project_kernel<float><<<pg, 256, 0, c->stream>>>(ea);
                 }
@@ -1231,6 +1437,8 @@ kb2e_status kb2e_profile_enable(kb2e_ctx* c, int32_t on) {
     return guarded(c, [&] {
         c->flush_timers();
         c->prof = on != 0;
+        c->prof_period = on > 1 ? on : 1;
+        c->prof_counter = 0;
         c->timers.clear();
         return KB2E_OK;
     });

@@ -68,6 +68,17 @@ struct GlibcRand {
         return val;
     }
 
+    // The 31 most recent raw words, oldest first (the word the next call adds
+    // to is w[0], lag 31; w[28] is lag 3).
+    void window(uint32_t w[kDeg]) const {
+        for (int m = 0; m < kDeg; ++m) w[m] = (uint32_t)state[(f + m) % kDeg];
+    }
+    void set_window(const uint32_t w[kDeg]) {
+        for (int m = 0; m < kDeg; ++m) state[m] = (int32_t)w[m];
+        f = 0;
+        r = kDeg - kSep;
+    }
+
     // Advance this generator past `m` words whose raw values `vals[0..m)` were
     // generated from exactly this state (f and r always move together, r = f - 3
     // mod 31, and the word made at step q lands in slot (f + q) mod 31).
@@ -82,6 +93,20 @@ struct GlibcRand {
         r = (f + kDeg - kSep) % kDeg;
     }
 };
+
+// Jump table of the TYPE_3 recurrence r[i] = r[i-3] + r[i-31] (mod 2^32):
+// r[i0 + t] = sum_m C[m][t] * r[i0 - 31 + m] for 0 <= t < L, stored m-major
+// (C[m * L + t]) so consecutive t are consecutive words.  With it the device
+// makes a whole epoch's words in parallel from one 31-word window.
+inline void glibc_jump_table(int L, uint32_t* C) {
+    constexpr int D = GlibcRand::kDeg;
+    // coef(t) for t >= -31: unit vectors before i0, then coef(t-3) + coef(t-31)
+    auto at = [&](int t, int m) -> uint32_t {
+        return t < 0 ? (uint32_t)(m == D + t ? 1u : 0u) : C[(size_t)m * L + t];
+    };
+    for (int t = 0; t < L; ++t)
+        for (int m = 0; m < D; ++m) C[(size_t)m * L + t] = at(t - GlibcRand::kSep, m) + at(t - D, m);
+}
 
 // common/utils.cpp:113-120 -- (rand() * rand()) % x in int32 with wrap-around
 // (the product overflows in practice; both factors are consumed either way).

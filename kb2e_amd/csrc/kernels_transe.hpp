@@ -24,7 +24,7 @@ struct ScoreArgs {
     const int32_t* si;  // sample stream of this batch (already offset)
     const int32_t* sj;
     const uint8_t* side;
-    int32_t B, n, ld, nw;
+    int32_t B, n, ld, nw, ne;
     const T* ent;
     const T* rel;
     const T* w;  // TransH normals (R x ld) / TransR matrices
@@ -35,11 +35,69 @@ struct ScoreArgs {
     T* xreal;           // [B][2][ld] (L2 only)
 };
 
-template <typename T, int CH, bool L1>
-__global__ __launch_bounds__(256) void transe_score_kernel(ScoreArgs<T> a) {
+// Per-event records written by phase A in sorted-event order (position p of
+// the epoch's event index): meta = (s + 1) | nn << 2 | (2 kk + u) << 4 with s
+// the sign of the event's delta (0: none) and nn its norm count; L1 also the
+// event's sign words.  Phase B then reads each segment's events contiguously.
+struct EventRecs {
+    int32_t* meta;     // [nkeys]
+    uint64_t* words;   // [nkeys][nw] (L1)
+    const int32_t* inv;       // unsorted slot -> sorted position
+    const uint64_t* keys;     // unsorted keys (emit order: sample * slots + slot)
+    const int32_t* seg_row;   // [nseg] row of each segment
+    int32_t slots;
+};
+
+__device__ __forceinline__ int32_t pack_meta(int sgn, int nn, int xrow) { return (sgn + 1) | (nn << 2) | (xrow << 4); }
+
+// Phase A side: lanes 0..slots-1 of the sample's wave write the records of the
+// sample's events (transe/trainer.cpp:36-40 signs: relation and head rows -d,
+// tail rows +d, d = (corrupted ? +1 : -1) lr x).  The slot's key and sorted
+// position are fetched at kernel start (prefetch) and used at the end (write).
+struct EventSlot {
+    uint64_t key = kSentinelKey;
+    int p = 0;
+    __device__ __forceinline__ void prefetch(const EventRecs& er, int64_t k) {
+        const int l = lane_id();
+        if (l < er.slots) {
+            key = er.keys[k * er.slots + l];
+            p = er.inv[k * er.slots + l];
+        }
+    }
+    template <int NW>
+    __device__ __forceinline__ void write(const EventRecs& er, const KeyLayout& kl, int32_t ne, int kk, bool active,
+                                          const uint64_t (&bp)[NW], const uint64_t (&bn)[NW], int nw) const {
+        if (key == kSentinelKey) return;
+        const int u = (int)((key >> 3) & 1);
+        const uint32_t roles = (uint32_t)(key & 7);
+        const bool is_rel = kl.row_of(key) >= ne;
+        int sgn = 0, nn = 0;
+        if (active) {
+            const int us = u ? 1 : -1;
+            if (is_rel) {
+                sgn = -us;
+                nn = 1;
+            } else {
+                const bool hd = roles & kRoleHead, tl = roles & kRoleTail;
+                sgn = (hd && tl) ? 0 : (hd ? -us : us);
+                nn = (hd ? 1 : 0) + (tl ? 1 : 0);
+            }
+            if (sgn != 0)
+                for (int w = 0; w < nw; ++w) er.words[(int64_t)p * nw + w] = u ? bn[w] : bp[w];
+        }
+        er.meta[p] = pack_meta(sgn, nn, kk * 2 + u);
+    }
+};
+
+// EMIT (PARALLEL schedule): also write the sample's event records.
+template <typename T, int CH, bool L1, bool EMIT = false>
+__global__ __launch_bounds__(256) void transe_score_kernel(ScoreArgs<T> a, EventRecs er = {}, KeyLayout kl = {},
+                                                           int64_t kbase = 0) {
     const int kk = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (kk >= a.B) return;
     const int l = lane_id();
+    EventSlot slot;
+    if (EMIT) slot.prefetch(er, kbase + kk);
     const int i = a.si[kk], j = a.sj[kk];
     const int h = a.heads[i], t = a.tails[i], r = a.rels[i];
     const int nh = a.side[kk] ? h : j, nt = a.side[kk] ? j : t;
@@ -74,7 +132,11 @@ __global__ __launch_bounds__(256) void transe_score_kernel(ScoreArgs<T> a) {
         a.act[kk] = active ? 1 : 0;
         a.loss[kk] = active ? a.margin + e_pos - e_neg : 0.0;
     }
-    if (!active) return;
+    uint64_t bpw[CH * kVec], bnw[CH * kVec];
+    if (!active) {
+        if (EMIT) slot.write<CH * kVec>(er, kl, a.ne, kk, false, bpw, bnw, a.nw);
+        return;
+    }
     if (L1) {
 #pragma unroll
         for (int c = 0; c < CH; ++c)
@@ -84,12 +146,16 @@ __global__ __launch_bounds__(256) void transe_score_kernel(ScoreArgs<T> a) {
                 const bool valid = elem_valid(c, k, a.n);
                 const uint64_t bp = __ballot(valid && dp[c][k] > T(0));
                 const uint64_t bn = __ballot(valid && dn[c][k] > T(0));
-                if (l == 0) {
+                bpw[c * kVec + k] = bp;
+                bnw[c * kVec + k] = bn;
+                if (!EMIT && l == 0) {
                     a.xbits[((int64_t)kk * 2 + 0) * a.nw + c * kVec + k] = bp;
                     a.xbits[((int64_t)kk * 2 + 1) * a.nw + c * kVec + k] = bn;
                 }
             }
+        if (EMIT) slot.write<CH * kVec>(er, kl, a.ne, kk, true, bpw, bnw, a.nw);
     } else {
+        if (EMIT) slot.write<CH * kVec>(er, kl, a.ne, kk, true, bpw, bnw, 0);
         T* xp = a.xreal + ((int64_t)kk * 2 + 0) * a.ld;
         T* xn = a.xreal + ((int64_t)kk * 2 + 1) * a.ld;
 #pragma unroll

@@ -1,0 +1,620 @@
+// kernels_transr_parallel.hpp -- TransR under the PARALLEL schedule
+// (KB2E_SCHEDULE_PARALLEL, see kernels_parallel.hpp for the TransE form).
+//
+// The reference's TransR step (transr/trainer.cpp:144-188) for one update u =
+// (h, t, r, beta) with snapshot W = weights_[r]:
+//   x = sign / 2 (W^T t - W^T h - r)                (L1 / L2; :147-164)
+//   W'  -= beta lr (h - t) x^T                        (:166-167)
+//   h'  -= beta lr W x,  t' += beta lr W x,  r' -= beta lr x   (:168-172)
+//   unit norms of r', h', t' and of every row of W'   (:174-180)
+//   transRNorm(h'), transRNorm(t'), transRNorm(entity'[r]) against W'  (:185-187)
+// The ORDERED schedule replays that per update (kernels_relowner.hpp).  Here a
+// batch is processed as:
+//   tile      per (relation, <= St samples): W_r staged in LDS; projections of
+//             h, t, h', t' (energies + hinge, or the compat work-vector scan),
+//             x, d = h - t, y = W x for both updates; the tile's partial sums
+//             dW = -lr sum beta d x^T and dr = -lr sum beta x.
+//   rel rows  one wave per (relation, row j of W or the relation vector): the
+//             tiles' partials in tile order, then the unit norm.
+//   entities  per entity segment of the event index: sum of -beta lr y (head
+//             role) / +beta lr y (tail role), then the unit norm.
+//   transRNorm one Jacobi step per batch: per tile, every (h', r), (t', r) pair
+//             of an active update and (entity'[r], r) once per relation with
+//             |W'^T a|^2 > 1 takes g = 2 W'^T a, dW -= lr a g^T, da = -lr W' g
+//             (the first column sweep of transRNorm's loop with the whole
+//             column set at once); then rel rows (no norm) and entities (no norm).
+// Every sum runs in a fixed order: deterministic.
+#pragma once
+
+#include "kernels_common.hpp"
+
+namespace kb2e {
+
+// One tile: samples [first, first + count) of relation segment `seg`.
+struct RTile {
+    int32_t seg, q;
+};
+
+struct RParArgs {
+    // batch
+    const int32_t* heads;
+    const int32_t* tails;
+    const int32_t* rels;
+    const int32_t* si;  // this batch's sample stream
+    const int32_t* sj;
+    const uint8_t* side;
+    int32_t B, n, ld, ne, nr, St;
+    int32_t batch;
+    double lr, margin;
+    int32_t compat, l1;
+    // event index
+    const uint64_t* keys;       // sorted
+    const int32_t* seg_start;
+    const int32_t* batch_seg;
+    const int32_t* seg_row;     // row of every segment
+    const int32_t* rel_begin;   // [nb] first relation segment of each batch
+    const int32_t* tile_first;  // [nseg + 1] first tile of each segment (exclusive scan of tile counts)
+    const RTile* tiles;
+    KeyLayout kl;
+    // per-sample exports
+    uint8_t* act;        // [B] of this batch
+    double* loss;        // [B]
+    double* proj;        // [B][2][2][ld] compat projections
+    int32_t* tile_act;   // [tiles] active updates per tile
+};
+
+template <typename T>
+struct RParBufs {
+    T* ent;
+    T* rel;
+    T* W;        // live matrices [r][j][ld]
+    T* x;        // [B][2][ld]
+    T* d;        // [B][2][ld] snapshot h - t
+    T* y;        // [B][2][ld] W x
+    T* wpart;    // [tiles][n][ld]
+    T* rpart;    // [tiles][ld]
+    T* pair;     // [B][2][2][ld] transRNorm deltas of (h, r), (t, r) per update
+    T* relpair;  // [R][ld] transRNorm delta of (entity[r], r)
+    uint32_t* relpair_stamp;  // [R] batch stamp when relpair[r] is valid this batch
+    uint32_t stamp;
+};
+
+template <typename T>
+__host__ __device__ constexpr int rpar_lds_w(int n, int ld) {
+    return n * ld;  // elements of one staged matrix
+}
+
+// Tile geometry: which samples (kk) a tile holds.  Relation segments list two
+// events (u = 0, 1) per sample in kk order.
+__device__ __forceinline__ void tile_range(const RParArgs& a, int t, int& r, int& e0, int& cnt) {
+    const RTile tl = a.tiles[t];
+    const int p0 = a.seg_start[tl.seg], p1 = a.seg_start[tl.seg + 1];
+    r = a.seg_row[tl.seg] - a.ne;
+    const int ns = (p1 - p0) / 2;
+    const int f = tl.q * a.St;
+    e0 = p0 + 2 * f;
+    cnt = min(a.St, ns - f);
+}
+
+template <typename T>
+__device__ __forceinline__ void stage_matrix(T* Wl, const T* Wg, int n, int ld) {
+    for (int idx = threadIdx.x; idx < n * ld; idx += blockDim.x) Wl[idx] = Wg[idx];
+}
+
+// p_i = sum_j W[j][i] v_j for four vectors at once, lane l owning i = 2l, 2l+1
+// (n <= 128); the vectors are read as LDS broadcasts.
+template <typename T>
+__device__ __forceinline__ void project4(const T* Wl, int ld, int n, const T* v4 /* [4][ld] */, T (&p)[4][2]) {
+    const int l = lane_id();
+    const int i = 2 * l;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) p[q][0] = p[q][1] = T(0);
+    if (i >= n) return;
+    for (int j = 0; j < n; ++j) {
+        const T w0 = Wl[j * ld + i], w1 = Wl[j * ld + i + 1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const T vj = v4[q * ld + j];
+            p[q][0] += w0 * vj;
+            p[q][1] += w1 * vj;
+        }
+    }
+}
+
+// y_j = sum_i W[j][i] x_i, lane l owning j = 2l, 2l+1 (x read as LDS broadcasts).
+template <typename T>
+__device__ __forceinline__ void matvec_rows(const T* Wl, int ld, int n, const T* xl, T (&y)[2]) {
+    const int l = lane_id();
+    const int j = 2 * l;
+    y[0] = y[1] = T(0);
+    if (j >= n) return;
+    const T* r0 = Wl + j * ld;
+    const T* r1 = Wl + (j + 1) * ld;
+    const bool has1 = j + 1 < n;
+    for (int i = 0; i < n; ++i) {
+        const T xi = xl[i];
+        y[0] += r0[i] * xi;
+        if (has1) y[1] += r1[i] * xi;
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void lane_pair_load(const T* row, int n, T (&v)[2]) {
+    const int e = 2 * lane_id();
+    v[0] = e < n ? row[e] : T(0);
+    v[1] = e + 1 < n ? row[e + 1] : T(0);
+}
+template <typename T>
+__device__ __forceinline__ void lane_pair_store(T* row, int n, const T (&v)[2]) {
+    const int e = 2 * lane_id();
+    if (e < n) row[e] = v[0];
+    if (e + 1 < n) row[e + 1] = v[1];
+}
+
+// rows [j0, j0 + rows) of the tile's partial  dW[j][i] = sum_u D[u][j] X[u][i]
+// (D already scaled by -lr beta, zero for inactive updates); lane l owns
+// columns i = 2l, 2l+1.
+template <typename T>
+__device__ __forceinline__ void rank_sum_rows(const T* Dl, const T* Xl, int U, int ld, int n, int j, T (&acc)[2]) {
+    const int i = 2 * lane_id();
+    acc[0] = acc[1] = T(0);
+    if (i >= n) return;
+    for (int u = 0; u < U; ++u) {
+        const T dj = Dl[u * ld + j];
+        acc[0] += dj * Xl[u * ld + i];
+        acc[1] += dj * Xl[u * ld + i + 1];
+    }
+}
+
+// LDS layout of the tile kernels (elements of T): W [n][ld] | per wave 4 x ld
+// vectors | X [4 St + 1][ld] | D [4 St + 1][ld] | coef [4 St + 1] | int [4 St + 1]
+template <typename T>
+__host__ __device__ constexpr size_t rpar_tile_lds(int n, int ld, int St) {
+    return sizeof(T) * ((size_t)n * ld + 4 * 4 * (size_t)ld + 2 * (4 * (size_t)St + 1) * ld + 4 * (size_t)St + 1) +
+           sizeof(int) * (4 * (size_t)St + 1);
+}
+
+// Tile phase A + gradient partials (non-compat: energies here; compat: the
+// energies come from the work-vector scan, so GRAD runs as its own launch).
+template <typename T, bool PROJ, bool GRAD>
+__global__ __launch_bounds__(256) void transr_tile_kernel(RParArgs a, RParBufs<T> bf) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int t = a.tile_first[a.batch_seg[a.batch]] + blockIdx.x;
+    if (t >= a.tile_first[a.batch_seg[a.batch + 1]]) return;
+    int r, e0, cnt;
+    tile_range(a, t, r, e0, cnt);
+    const int n = a.n, ld = a.ld;
+    T* Wl = (T*)smem;
+    T* vec = Wl + n * ld;                  // [4 waves][4][ld]
+    T* Xl = vec + 16 * ld;                 // [2 cnt][ld] update directions
+    T* Dl = Xl + (4 * a.St + 1) * ld;      // [2 cnt][ld] -lr beta (h - t), 0 if inactive
+    T* coef = Dl + (4 * a.St + 1) * ld;    // [2 cnt] -lr beta, 0 if inactive
+    const int w = threadIdx.x >> 6, l = lane_id();
+    stage_matrix(Wl, bf.W + (int64_t)r * n * ld, n, ld);
+    __syncthreads();
+    T* v4 = vec + w * 4 * ld;
+    for (int q = w; q < cnt; q += 4) {
+        const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
+        if (PROJ) {
+            const int i0 = a.si[kk], jj = a.sj[kk];
+            const int h = a.heads[i0], tt = a.tails[i0];
+            const int nh = a.side[kk] ? h : jj, nt = a.side[kk] ? jj : tt;
+            T vh[2], vt[2], vnh[2], vnt[2], vr[2];
+            lane_pair_load(bf.ent + (int64_t)h * ld, n, vh);
+            lane_pair_load(bf.ent + (int64_t)tt * ld, n, vt);
+            lane_pair_load(bf.ent + (int64_t)nh * ld, n, vnh);
+            lane_pair_load(bf.ent + (int64_t)nt * ld, n, vnt);
+            lane_pair_load(bf.rel + (int64_t)r * ld, n, vr);
+            lane_pair_store(v4 + 0 * ld, n, vh);
+            lane_pair_store(v4 + 1 * ld, n, vt);
+            lane_pair_store(v4 + 2 * ld, n, vnh);
+            lane_pair_store(v4 + 3 * ld, n, vnt);
+            wave_lds_sync();
+            T p[4][2];
+            project4(Wl, ld, n, v4, p);  // W^T h, W^T t, W^T h', W^T t'
+            T ep = T(0), en = T(0);
+            T xp[2], xn[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const bool ok = 2 * l + k < n;
+                const T dp = p[1][k] - p[0][k] - vr[k];
+                const T dn = p[3][k] - p[2][k] - vr[k];
+                ep += ok ? (a.l1 ? fabs(dp) : dp * dp) : T(0);
+                en += ok ? (a.l1 ? fabs(dn) : dn * dn) : T(0);
+                xp[k] = ok ? (a.l1 ? (dp > T(0) ? T(1) : T(-1)) : T(2) * dp) : T(0);
+                xn[k] = ok ? (a.l1 ? (dn > T(0) ? T(1) : T(-1)) : T(2) * dn) : T(0);
+            }
+            const T dpos[2] = {vh[0] - vt[0], vh[1] - vt[1]};
+            const T dneg[2] = {vnh[0] - vnt[0], vnh[1] - vnt[1]};
+            lane_pair_store(bf.x + ((int64_t)kk * 2 + 0) * ld, n, xp);
+            lane_pair_store(bf.x + ((int64_t)kk * 2 + 1) * ld, n, xn);
+            lane_pair_store(bf.d + ((int64_t)kk * 2 + 0) * ld, n, dpos);
+            lane_pair_store(bf.d + ((int64_t)kk * 2 + 1) * ld, n, dneg);
+            if (a.compat) {
+                double* pr = a.proj + (int64_t)kk * 4 * ld;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int e = 2 * l + k;
+                    if (e >= n) continue;
+                    pr[e] = (double)p[0][k];
+                    pr[ld + e] = (double)p[1][k];
+                    pr[2 * ld + e] = (double)p[2][k];
+                    pr[3 * ld + e] = (double)p[3][k];
+                }
+            } else {
+                ep = wave_sum(ep);
+                en = wave_sum(en);
+                const bool active = (double)ep + a.margin > (double)en;
+                if (l == 0) {
+                    a.act[kk] = active ? 1 : 0;
+                    a.loss[kk] = active ? a.margin + (double)ep - (double)en : 0.0;
+                }
+                if (GRAD) {  // the tile's gradient rows, straight to LDS
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const T c = active ? (T)(-(u ? 1.0 : -1.0) * a.lr) : T(0);  // -lr beta
+                        const T* dv = u ? dneg : dpos;
+                        const T dsc[2] = {c * dv[0], c * dv[1]};
+                        lane_pair_store(Xl + (2 * q + u) * ld, n, u ? xn : xp);
+                        lane_pair_store(Dl + (2 * q + u) * ld, n, dsc);
+                        if (l == 0) coef[2 * q + u] = c;
+                    }
+                }
+            }
+            // y = W x for both updates (x through LDS)
+            wave_lds_sync();
+            lane_pair_store(v4 + 0 * ld, n, xp);
+            lane_pair_store(v4 + 1 * ld, n, xn);
+            wave_lds_sync();
+            T yp[2], yn[2];
+            matvec_rows(Wl, ld, n, v4 + 0 * ld, yp);
+            matvec_rows(Wl, ld, n, v4 + 1 * ld, yn);
+            lane_pair_store(bf.y + ((int64_t)kk * 2 + 0) * ld, n, yp);
+            lane_pair_store(bf.y + ((int64_t)kk * 2 + 1) * ld, n, yn);
+            wave_lds_sync();
+        }
+    }
+    if (!GRAD) return;
+    if (!PROJ) {  // compat: directions from phase A, hinge from the work-vector scan
+        for (int q = w; q < cnt; q += 4) {
+            const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
+            const bool act = a.act[kk] != 0;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const T c = act ? (T)(-(u ? 1.0 : -1.0) * a.lr) : T(0);  // -lr beta
+                T xv[2], dv[2];
+                lane_pair_load(bf.x + ((int64_t)kk * 2 + u) * ld, n, xv);
+                lane_pair_load(bf.d + ((int64_t)kk * 2 + u) * ld, n, dv);
+                dv[0] *= c;
+                dv[1] *= c;
+                lane_pair_store(Xl + (2 * q + u) * ld, n, xv);
+                lane_pair_store(Dl + (2 * q + u) * ld, n, dv);
+                if (l == 0) coef[2 * q + u] = c;
+            }
+        }
+    }
+    __syncthreads();
+    const int U = 2 * cnt;
+    T* wp = bf.wpart + (int64_t)blockIdx.x * n * ld;  // partials are per batch: local tile index
+    for (int j = w; j < n; j += 4) {  // dW = sum_u (-lr beta) (h - t) x^T
+        T acc[2];
+        rank_sum_rows(Dl, Xl, U, ld, n, j, acc);
+        lane_pair_store(wp + (int64_t)j * ld, n, acc);
+    }
+    if (w == 0) {  // dr = sum_u (-lr beta) x_u
+        T acc[2] = {T(0), T(0)};
+        const int i = 2 * l;
+        for (int u = 0; u < U; ++u) {
+            const T c = coef[u];
+            if (i < n) acc[0] += c * Xl[u * ld + i];
+            if (i + 1 < n) acc[1] += c * Xl[u * ld + i + 1];
+        }
+        lane_pair_store(bf.rpart + (int64_t)blockIdx.x * ld, n, acc);
+        if (l == 0) {
+            int nact = 0;
+            for (int u = 0; u < U; ++u) nact += coef[u] != T(0);
+            a.tile_act[t] = nact;
+        }
+    }
+}
+// One wave per (relation segment, row j <= n) of the batch: the tiles' partials
+// in tile order added to row j of W_r (j < n) or to the relation vector (j == n),
+// then the unit norm (common::norm(v, false), transr/trainer.cpp:174-180) when
+// NORM.  Without NORM (the transRNorm step) only the matrix rows change.
+template <typename T, bool NORM>
+__global__ __launch_bounds__(256) void transr_rel_rows_kernel(RParArgs a, RParBufs<T> bf) {
+    const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int rows = a.n + 1;
+    const int s = a.rel_begin[a.batch] + gw / rows;
+    const int j = gw % rows;
+    if (s >= a.batch_seg[a.batch + 1]) return;
+    if (!NORM && j == a.n) return;
+    const int r = a.seg_row[s] - a.ne;
+    const int t0 = a.tile_first[s], t1 = a.tile_first[s + 1];
+    const int n = a.n, ld = a.ld;
+    int any = 0;  // the reference touches (and normalises) a relation only through an active update
+    for (int t = t0; t < t1; ++t) any |= a.tile_act[t];
+    if (!any) return;
+    T* row = j < n ? bf.W + ((int64_t)r * n + j) * ld : bf.rel + (int64_t)r * ld;
+    T v[2];
+    lane_pair_load(row, n, v);
+    const int tb = a.tile_first[a.batch_seg[a.batch]];  // partials are indexed by tile within the batch
+    for (int t = t0; t < t1; ++t) {
+        T p[2];
+        const int64_t lt = t - tb;
+        lane_pair_load(j < n ? bf.wpart + (lt * n + j) * ld : bf.rpart + lt * ld, n, p);
+        v[0] += p[0];
+        v[1] += p[1];
+    }
+    if (NORM) {
+        const T len = sqrt(wave_sum(v[0] * v[0] + v[1] * v[1]));
+        v[0] = v[0] / len;
+        v[1] = v[1] / len;
+    }
+    lane_pair_store(row, n, v);
+}
+
+// transRNorm (transr/trainer.cpp:35-64) per tile, on W'_r and the entity rows
+// after the batch's gradient step.  Pairs: (h', r), (t', r) of the tile's
+// active updates and (entity'[r], r) on the relation's first tile; a pair
+// whose entity already occurs earlier in the tile is the reference's repeated
+// call on an already constrained row, a no-op to first order, and is skipped.
+// Per pair, with W0 = W'_r and the loop run in Jacobi form (all columns at
+// once) while |p|^2 > 1 (p = W^T a):
+//   g_m = 2 p_m,  a_{m+1} = a_m - lr W0 g_m,
+//   p_{m+1} = W0^T a_{m+1} - lr (a0.a0) sum_{k<=m} g_k   (W's own shrink, to first order),
+// then da = a_K - a0 (pair record) and the matrix step -lr a0 (sum_m g_m)^T
+// (tile partial; exact to first order in lr).
+constexpr int kRParMaxIter = 256;
+
+template <typename T>
+__global__ __launch_bounds__(256) void transr_constraint_kernel(RParArgs a, RParBufs<T> bf) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int t = a.tile_first[a.batch_seg[a.batch]] + blockIdx.x;
+    if (t >= a.tile_first[a.batch_seg[a.batch + 1]]) return;
+    int r, e0, cnt;
+    tile_range(a, t, r, e0, cnt);
+    const int n = a.n, ld = a.ld;
+    T* Wl = (T*)smem;
+    T* vec = Wl + n * ld;
+    T* Xl = vec + 16 * ld;                // sum of g per pair   [4 cnt + 1][ld]
+    T* Dl = Xl + (4 * a.St + 1) * ld;     // -lr a0 per pair     [4 cnt + 1][ld]
+    int* ent_of = (int*)(Dl + (4 * a.St + 1) * ld + 4 * a.St + 1);  // [4 cnt + 1] entity of each pair slot
+    const int w = threadIdx.x >> 6, l = lane_id();
+    const RTile tl = a.tiles[t];
+    bool relpair = false;  // the relation-level pair rides on the first tile
+    if (tl.q == 0) {
+        int any = 0;
+        for (int q = a.tile_first[tl.seg]; q < a.tile_first[tl.seg + 1]; ++q) any |= a.tile_act[q];
+        relpair = any != 0 && r < a.ne;
+    }
+    const int npairs = 4 * cnt + (relpair ? 1 : 0);  // slots (q, u, role), then entity[r]
+    for (int pq = threadIdx.x; pq < npairs; pq += blockDim.x) {
+        int ent = -1;
+        if (pq < 4 * cnt) {
+            const int q = pq >> 2, u = (pq >> 1) & 1, role = pq & 1;
+            const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
+            if (a.act[kk]) {
+                const int i0 = a.si[kk], jj = a.sj[kk];
+                const int h = a.heads[i0], tt = a.tails[i0];
+                const int hh = u ? (a.side[kk] ? h : jj) : h;
+                const int th = u ? (a.side[kk] ? jj : tt) : tt;
+                ent = role ? th : hh;
+            }
+        } else {
+            ent = r;  // entityVec_next_[relation] (transr/trainer.cpp:187)
+        }
+        ent_of[pq] = ent;
+    }
+    stage_matrix(Wl, bf.W + (int64_t)r * n * ld, n, ld);
+    __syncthreads();
+    T* v4 = vec + w * 4 * ld;
+    const int i = 2 * l;
+    for (int pq = w; pq < npairs; pq += 4) {
+        const int ent = ent_of[pq];
+        bool live = ent >= 0;
+        for (int k = 0; live && k < pq; ++k) live = ent_of[k] != ent;  // first occurrence only
+        T a0[2] = {T(0), T(0)}, av[2], G[2] = {T(0), T(0)};
+        if (live) {
+            lane_pair_load(bf.ent + (int64_t)ent * ld, n, a0);
+            av[0] = a0[0];
+            av[1] = a0[1];
+            const T s0 = wave_sum(a0[0] * a0[0] + a0[1] * a0[1]);
+            for (int m = 0; m < kRParMaxIter; ++m) {
+                lane_pair_store(v4, n, av);
+                wave_lds_sync();
+                T p[2] = {T(0), T(0)};
+                if (i < n)
+                    for (int j = 0; j < n; ++j) {
+                        const T aj = v4[j];
+                        p[0] += Wl[j * ld + i] * aj;
+                        p[1] += Wl[j * ld + i + 1] * aj;
+                    }
+                const T ws = T(a.lr) * s0;
+                p[0] -= ws * G[0];
+                p[1] -= ws * G[1];
+                if (i + 1 >= n) p[1] = T(0);
+                if (i >= n) p[0] = T(0);
+                const T xx = wave_sum(p[0] * p[0] + p[1] * p[1]);
+                if (!(xx > T(1))) break;
+                const T g[2] = {T(2) * p[0], T(2) * p[1]};
+                G[0] += g[0];
+                G[1] += g[1];
+                lane_pair_store(v4 + ld, n, g);
+                wave_lds_sync();
+                T y[2];
+                matvec_rows(Wl, ld, n, v4 + ld, y);  // W0 g
+                av[0] -= T(a.lr) * y[0];
+                av[1] -= T(a.lr) * y[1];
+                wave_lds_sync();
+            }
+        }
+        const T da[2] = {live ? av[0] - a0[0] : T(0), live ? av[1] - a0[1] : T(0)};
+        if (pq < 4 * cnt) {
+            const int q = pq >> 2, u = (pq >> 1) & 1, role = pq & 1;
+            const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
+            if (a.act[kk]) lane_pair_store(bf.pair + (((int64_t)kk * 2 + u) * 2 + role) * ld, n, da);
+        } else {
+            lane_pair_store(bf.relpair + (int64_t)r * ld, n, da);
+            if (l == 0) bf.relpair_stamp[r] = bf.stamp;
+        }
+        const T dv[2] = {T(-a.lr) * a0[0], T(-a.lr) * a0[1]};
+        lane_pair_store(Xl + pq * ld, n, G);
+        lane_pair_store(Dl + pq * ld, n, dv);
+    }
+    __syncthreads();
+    T* wp = bf.wpart + (int64_t)blockIdx.x * n * ld;
+    for (int j = w; j < n; j += 4) {
+        T acc[2];
+        rank_sum_rows(Dl, Xl, npairs, ld, n, j, acc);
+        lane_pair_store(wp + (int64_t)j * ld, n, acc);
+    }
+}
+
+// Entity rows, per entity segment of the batch (one wave; long segments a
+// 1024-thread workgroup).  GRAD: head role -beta lr y, tail role +beta lr y
+// (transr/trainer.cpp:168-169), then the unit norm (:175-176) if an active
+// update used the row as head or tail.  !GRAD: the transRNorm pair deltas
+// (and the (entity[r], r) delta once), no norm.
+constexpr int kRParWaves = 16;
+
+template <typename T, bool GRAD>
+__device__ __forceinline__ void rpar_entity_events(const RParArgs& a, const RParBufs<T>& bf, int row, int p0, int p1,
+                                                   int first, int stride, T (&acc)[2], bool& dirty, bool& er_seen) {
+    const int n = a.n, ld = a.ld;
+    for (int p = p0 + first; p < p1; p += stride) {
+        const uint64_t key = a.keys[p];
+        const int kk = a.kl.kk_of(key);
+        if (!a.act[kk]) continue;
+        const int u = (int)((key >> 3) & 1);
+        const uint32_t roles = (uint32_t)(key & 7);
+        const bool hd = roles & kRoleHead, tl = roles & kRoleTail;
+        if (GRAD) {
+            if (!hd && !tl) continue;
+            dirty = true;
+            if (hd && tl) continue;  // -beta lr y + beta lr y
+            const T c = (T)((hd ? -1.0 : 1.0) * (u ? 1.0 : -1.0) * a.lr);
+            T yv[2];
+            lane_pair_load(bf.y + ((int64_t)kk * 2 + u) * ld, n, yv);
+            acc[0] += c * yv[0];
+            acc[1] += c * yv[1];
+        } else {
+            if (roles & kRoleEntRel) er_seen = true;
+#pragma unroll
+            for (int role = 0; role < 2; ++role) {
+                if (!(role ? tl : hd)) continue;
+                T dv[2];
+                lane_pair_load(bf.pair + (((int64_t)kk * 2 + u) * 2 + role) * ld, n, dv);
+                acc[0] += dv[0];
+                acc[1] += dv[1];
+                dirty = true;
+            }
+        }
+    }
+}
+
+template <typename T, bool GRAD>
+__device__ __forceinline__ void rpar_entity_finish(const RParArgs& a, const RParBufs<T>& bf, int row, T (&acc)[2],
+                                                   bool dirty, bool er_seen) {
+    const int n = a.n, ld = a.ld;
+    if (!GRAD && er_seen && row < a.nr && bf.relpair_stamp[row] == bf.stamp) {
+        T dv[2];
+        lane_pair_load(bf.relpair + (int64_t)row * ld, n, dv);
+        acc[0] += dv[0];
+        acc[1] += dv[1];
+        dirty = true;
+    }
+    if (!dirty) return;
+    T* ptr = bf.ent + (int64_t)row * ld;
+    T v[2];
+    lane_pair_load(ptr, n, v);
+    v[0] += acc[0];
+    v[1] += acc[1];
+    if (GRAD) {
+        const T len = sqrt(wave_sum(v[0] * v[0] + v[1] * v[1]));
+        v[0] = v[0] / len;
+        v[1] = v[1] / len;
+    }
+    lane_pair_store(ptr, n, v);
+}
+
+template <typename T, bool GRAD>
+__global__ __launch_bounds__(1024) void transr_entity_kernel(RParArgs a, RParBufs<T> bf, int32_t long_min) {
+    __shared__ T part[kRParWaves][2][kWave];
+    __shared__ int flags[2];
+    const int w = threadIdx.x >> 6, l = lane_id();
+    const int s0 = a.batch_seg[a.batch], s1 = a.rel_begin[a.batch];  // entity segments sort first
+    const int G = gridDim.x;
+    // long segments: whole workgroup, segments s0 + blockIdx.x, s0 + blockIdx.x + G, ... that are long
+    for (int s = s0 + blockIdx.x; s < s1; s += G) {
+        const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
+        if (p1 - p0 < long_min) continue;
+        const int row = a.seg_row[s];
+        if (threadIdx.x < 2) flags[threadIdx.x] = 0;
+        __syncthreads();
+        T acc[2] = {T(0), T(0)};
+        bool dirty = false, er = false;
+        rpar_entity_events<T, GRAD>(a, bf, row, p0, p1, w, kRParWaves, acc, dirty, er);
+        part[w][0][l] = acc[0];
+        part[w][1][l] = acc[1];
+        if (l == 0 && dirty) atomicOr(&flags[0], 1);
+        if (l == 0 && er) atomicOr(&flags[1], 1);
+        __syncthreads();
+        if (w == 0) {
+            acc[0] = part[0][0][l];
+            acc[1] = part[0][1][l];
+            for (int v = 1; v < kRParWaves; ++v) {
+                acc[0] += part[v][0][l];
+                acc[1] += part[v][1][l];
+            }
+            rpar_entity_finish<T, GRAD>(a, bf, row, acc, flags[0] != 0, flags[1] != 0);
+        }
+        __syncthreads();
+    }
+    // short segments: one wave each
+    for (int s = s0 + blockIdx.x * kRParWaves + w; s < s1; s += G * kRParWaves) {
+        const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
+        if (p1 - p0 >= long_min) continue;
+        const int row = a.seg_row[s];
+        T acc[2] = {T(0), T(0)};
+        bool dirty = false, er = false;
+        rpar_entity_events<T, GRAD>(a, bf, row, p0, p1, 0, 1, acc, dirty, er);
+        rpar_entity_finish<T, GRAD>(a, bf, row, acc, dirty, er);
+    }
+}
+
+// ---- per-epoch tile index --------------------------------------------------
+
+// Tiles per segment (relation segments: ceil(samples / St); entity segments 0),
+// and the first relation segment of every batch.
+__global__ __launch_bounds__(256) void rtile_count_kernel(const uint64_t* keys, const int32_t* seg_start,
+                                                          const int32_t* nseg_p, int64_t cap, KeyLayout kl,
+                                                          int32_t ne, int32_t St, int32_t* ntiles,
+                                                          int32_t* rel_begin) {
+    const int nseg = *nseg_p;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += (int64_t)gridDim.x * blockDim.x) {
+        if (s >= nseg) {
+            ntiles[s] = 0;
+            continue;
+        }
+        const uint64_t k = keys[seg_start[s]];
+        const int row = kl.row_of(k);
+        const bool isrel = row >= ne;
+        const int ns = (seg_start[s + 1] - seg_start[s]) / 2;
+        ntiles[s] = isrel ? (ns + St - 1) / St : 0;
+        if (isrel) {
+            const bool first = s == 0 || kl.batch_of(keys[seg_start[s - 1]]) != kl.batch_of(k) ||
+                               kl.row_of(keys[seg_start[s - 1]]) < ne;
+            if (first) rel_begin[kl.batch_of(k)] = (int32_t)s;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void rtile_scatter_kernel(const int32_t* ntiles, const int32_t* tile_first,
+                                                            const int32_t* nseg_p, RTile* tiles) {
+    const int nseg = *nseg_p;
+    for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x)
+        for (int q = 0; q < ntiles[s]; ++q) tiles[tile_first[s] + q] = RTile{s, q};
+}
+
+}  // namespace kb2e

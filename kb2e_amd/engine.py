@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("KB2E_LIB") or os.path.join(HERE, "libkb2e.so")
 MODELS = {"transe": 0, "transh": 1, "transr": 2, "E": 0, "H": 1, "R": 2}
 STATUS = {0: "OK", 1: "EINVAL", 2: "EDEVICE", 3: "ESTATE", 4: "ENOMEM", 5: "EUNSUPPORTED", 6: "ESAMPLER"}
 SAMPLER_GLIBC, SAMPLER_REPLAY = 0, 1
+SCHEDULES = {"ordered": 0, "parallel": 1}
 
 # Every symbol include/kb2e_engine.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -33,7 +34,7 @@ class Config(C.Structure):
         ("model", C.c_int32), ("dim", C.c_int32), ("num_entities", C.c_int32), ("num_relations", C.c_int32),
         ("learning_rate", C.c_double), ("margin", C.c_double), ("method", C.c_int32), ("distance", C.c_int32),
         ("num_batches", C.c_int32), ("seed", C.c_uint32), ("precision", C.c_int32), ("sampler", C.c_int32),
-        ("transr_compat", C.c_int32), ("device", C.c_int32),
+        ("transr_compat", C.c_int32), ("device", C.c_int32), ("schedule", C.c_int32),
     ]
 
 
@@ -100,7 +101,7 @@ class Engine:
 
     def __init__(self, model, dim, num_entities, num_relations, *, rate=0.001, margin=1.0, method=1,
                  distance=0, batches=100, seed=0, precision=64, sampler=SAMPLER_GLIBC, transr_compat=True,
-                 device=0):
+                 device=0, schedule="ordered"):
         self.kind = MODELS[model] if isinstance(model, str) else int(model)
         self.n, self.ne, self.nr = dim, num_entities, num_relations
         cfg = Config()
@@ -109,6 +110,7 @@ class Engine:
         cfg.learning_rate, cfg.margin, cfg.method, cfg.distance = rate, margin, method, distance
         cfg.num_batches, cfg.seed, cfg.precision, cfg.sampler = batches, seed, precision, sampler
         cfg.transr_compat, cfg.device = int(transr_compat), device
+        cfg.schedule = SCHEDULES[schedule] if isinstance(schedule, str) else int(schedule)
         self.cfg = cfg
         h = C.c_void_p()
         st = lib().kb2e_create(C.byref(cfg), C.byref(h))
@@ -211,6 +213,7 @@ class Engine:
         return lib().kb2e_rng_next(self.h)
 
     def profile(self, on=True):
+        """on: False/0 off, True/1 every batch, P > 1 every P-th batch."""
         self._check(lib().kb2e_profile_enable(self.h, int(on)), "profile_enable")
 
     def profile_query(self, name):

@@ -1,0 +1,186 @@
+"""CPU model of the engine's PARALLEL schedule (TEST INFRASTRUCTURE ONLY).
+
+The PARALLEL schedule (include/kb2e_engine.h KB2E_SCHEDULE_PARALLEL,
+kb2e_amd/csrc/kernels_parallel.hpp) is not the reference's algorithm: it keeps
+the reference's sample stream, snapshot energies, hinge decisions and update
+directions (common/trainer.cpp:130-149, transe/trainer.cpp:24-46) and replaces
+the per-update renormalisation sequence with one summed delta + one
+common::norm per touched row and batch.  This module restates that relaxation
+in numpy on top of the C oracle's sample stream, so tests can check the GPU
+kernels element by element.  Only tests/ import it.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def _norm_rows(tab: np.ndarray, rows: np.ndarray, ignore_short: bool = True) -> None:
+    """common::norm (common/utils.cpp:70-77) on the listed rows."""
+    if rows.size == 0:
+        return
+    v = tab[rows]
+    ln = np.sqrt((v * v).sum(axis=1))
+    scale = (ln > 1.0) if ignore_short else np.ones_like(ln, dtype=bool)
+    v[scale] = v[scale] / ln[scale, None]
+    tab[rows] = v
+
+
+def transe_parallel_batches(ent, rel, triples, si, sj, side, B, nbatches, *, rate, margin=1.0, l1=True):
+    """Train `nbatches` TransE batches of the PARALLEL schedule in place.
+
+    Returns (loss, active).  Per batch: energies and directions from the
+    start-of-batch tables (transe/transe.cpp:10-28, transe/trainer.cpp:27-35);
+    deltas summed per row (L1: integer sign counts, as the kernel); then
+    row <- norm(row + rate * sum) for every row an active update touched.
+    """
+    loss = 0.0
+    active = 0
+    h_all, t_all, r_all = triples[:, 0], triples[:, 1], triples[:, 2]
+    for b in range(nbatches):
+        sl = slice(b * B, (b + 1) * B)
+        i, j, sd = si[sl], sj[sl], side[sl].astype(bool)
+        h, t, r = h_all[i], t_all[i], r_all[i]
+        nh = np.where(sd, h, j)
+        nt = np.where(sd, j, t)
+        dp = ent[t] - ent[h] - rel[r]
+        dn = ent[nt] - ent[nh] - rel[r]
+        ep = np.abs(dp).sum(1) if l1 else (dp * dp).sum(1)
+        en = np.abs(dn).sum(1) if l1 else (dn * dn).sum(1)
+        act = ep + margin > en
+        loss += float((margin + ep - en)[act].sum())
+        active += int(act.sum())
+        if l1:
+            xp = np.where(dp > 0, 1, -1).astype(np.int64)
+            xn = np.where(dn > 0, 1, -1).astype(np.int64)
+            acc_e = np.zeros(ent.shape, np.int64)
+            acc_r = np.zeros(rel.shape, np.int64)
+        else:
+            xp, xn = 2.0 * dp, 2.0 * dn
+            acc_e = np.zeros(ent.shape)
+            acc_r = np.zeros(rel.shape)
+        a = np.nonzero(act)[0]
+        # modifier: -1 for the training triple, +1 for the corrupted one
+        # (transe/trainer.cpp:25, 38-40): rel -= m lr x, head -= m lr x, tail += m lr x
+        for (hh, tt, xx, m) in ((h[a], t[a], xp[a], -1), (nh[a], nt[a], xn[a], 1)):
+            np.add.at(acc_r, r[a], -m * xx)
+            np.add.at(acc_e, hh, -m * xx)
+            np.add.at(acc_e, tt, m * xx)
+        er = np.unique(np.concatenate([h[a], t[a], nh[a], nt[a]]))
+        rr = np.unique(r[a])
+        ent[er] = ent[er] + rate * acc_e[er]
+        rel[rr] = rel[rr] + rate * acc_r[rr]
+        _norm_rows(ent, er)
+        _norm_rows(rel, rr)
+    return loss, active
+
+
+def transr_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, rate, margin=1.0, l1=True,
+                            compat=False, work=None, St=32, constraint=True):
+    """Train `nbatches` TransR batches of the PARALLEL schedule in place
+    (kb2e_amd/csrc/kernels_transr_parallel.hpp).  Returns (loss, active).
+
+    Per batch, from the start-of-batch tables (transr/trainer.cpp:144-188):
+    projections, energies (compat: the reference's accumulating work vectors,
+    transr/transr.cpp:20-25, carried in `work` = [head, tail]), hinge, x, d =
+    h - t, y = W x; summed dW, dr per relation, summed entity deltas; unit
+    norms; then one Jacobi step of transRNorm (transr/trainer.cpp:35-64) on
+    every (h', r), (t', r) pair of an active update and (entity'[r], r) once per
+    relation, iterated while |W^T a|^2 > 1, per tile of St samples.
+    """
+    loss = 0.0
+    active = 0
+    h_all, t_all, r_all = triples[:, 0], triples[:, 1], triples[:, 2]
+    for b in range(nbatches):
+        sl = slice(b * B, (b + 1) * B)
+        i, j, sd = si[sl], sj[sl], side[sl].astype(bool)
+        h, t, r = h_all[i], t_all[i], r_all[i]
+        nh = np.where(sd, h, j)
+        nt = np.where(sd, j, t)
+        Wr = W[r]                                   # [B][j][i]
+        proj = lambda v: np.einsum("kji,kj->ki", Wr, ent[v])
+        ph, pt, pnh, pnt = proj(h), proj(t), proj(nh), proj(nt)
+        R = rel[r]
+        if compat:
+            calls_h = np.stack([ph, pnh], 1).reshape(-1, ph.shape[1])
+            calls_t = np.stack([pt, pnt], 1).reshape(-1, pt.shape[1])
+            hw = work[0] + np.cumsum(calls_h, axis=0)
+            tw = work[1] + np.cumsum(calls_t, axis=0)
+            work[0], work[1] = hw[-1].copy(), tw[-1].copy()
+            dpe = (tw[0::2] - hw[0::2]) - R
+            dne = (tw[1::2] - hw[1::2]) - R
+        else:
+            dpe, dne = (pt - ph) - R, (pnt - pnh) - R
+        ep = np.abs(dpe).sum(1) if l1 else (dpe * dpe).sum(1)
+        en = np.abs(dne).sum(1) if l1 else (dne * dne).sum(1)
+        act = ep + margin > en
+        loss += float((margin + ep - en)[act].sum())
+        active += int(act.sum())
+        dp, dn = (pt - ph) - R, (pnt - pnh) - R    # fresh projections (transr/trainer.cpp:147-157)
+        xp = np.where(dp > 0, 1.0, -1.0) if l1 else 2.0 * dp
+        xn = np.where(dn > 0, 1.0, -1.0) if l1 else 2.0 * dn
+        a = np.nonzero(act)[0]
+        ups = [(h[a], t[a], xp[a], rate), (nh[a], nt[a], xn[a], -rate)]  # c = -lr beta
+        dW = np.zeros_like(W)
+        dr = np.zeros_like(rel)
+        acc = np.zeros_like(ent)
+        Wsnap = W.copy()
+        for (hh, tt, xx, c) in ups:
+            d = ent[hh] - ent[tt]
+            np.add.at(dW, r[a], c * np.einsum("kj,ki->kji", d, xx))
+            np.add.at(dr, r[a], c * xx)
+            y = np.einsum("kji,ki->kj", Wsnap[r[a]], xx)
+            np.add.at(acc, hh, c * y)
+            np.add.at(acc, tt, -c * y)
+        ra = np.unique(r[a])
+        W[ra] += dW[ra]
+        rel[ra] += dr[ra]
+        rel[ra] /= np.sqrt((rel[ra] ** 2).sum(1, keepdims=True))
+        W[ra] /= np.sqrt((W[ra] ** 2).sum(2, keepdims=True))
+        ea = np.unique(np.concatenate([h[a], t[a], nh[a], nt[a]]))
+        ent[ea] += acc[ea]
+        ent[ea] /= np.sqrt((ent[ea] ** 2).sum(1, keepdims=True))
+        if constraint:
+            transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St)
+    return loss, active
+
+
+def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St, dedupe=True, relpair=True, max_iter=256):
+    """transRNorm step of the PARALLEL TransR schedule, in place.
+
+    Per tile (relation, St samples in kk order): pairs (h', r), (t', r) of the
+    active updates in (sample, update, role) order, then (entity'[r], r) on the
+    relation's first tile; first occurrences only; the loop in Jacobi form to
+    first order (kernels_transr_parallel.hpp, transr_constraint_kernel).
+    """
+    ra = np.unique(r[act])
+    W0 = W.copy()
+    E1 = ent.copy()
+    dWc = np.zeros_like(W)
+    for rr in ra:
+        ks = np.nonzero(r == rr)[0]
+        for f in range(0, len(ks), St):
+            slots = []
+            for kk in ks[f:f + St]:
+                for (hh, tt) in ((h[kk], t[kk]), (nh[kk], nt[kk])):
+                    slots += [hh, tt] if act[kk] else [-1, -1]
+            if relpair and f == 0 and rr < ent.shape[0]:
+                slots.append(rr)
+            seen = set()
+            for e in slots:
+                if e < 0 or (dedupe and e in seen):
+                    continue
+                seen.add(e)
+                a0 = E1[e]
+                av = a0.copy()
+                G = np.zeros_like(a0)
+                s0 = a0 @ a0
+                for _ in range(max_iter):
+                    p = W0[rr].T @ av - rate * s0 * G
+                    if not (p @ p > 1.0):
+                        break
+                    g = 2.0 * p
+                    G += g
+                    av = av - rate * (W0[rr] @ g)
+                ent[e] += av - a0
+                dWc[rr] += np.outer(-rate * a0, G)
+    W[ra] += dWc[ra]

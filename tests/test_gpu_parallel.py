@@ -1,0 +1,123 @@
+"""PARALLEL schedule on the GPU vs its CPU model (oracle/parallel.py).
+
+The schedule keeps the reference's sample stream, snapshot energies, hinge
+decisions and update directions and applies each touched row's summed delta
+plus one norm per batch (include/kb2e_engine.h KB2E_SCHEDULE_PARALLEL).  The
+CPU model follows the same arithmetic (L1 deltas as integer sign counts), so
+the bar is the ulp-level difference of the 64-lane sums in the norms:
+1e-11 absolute per epoch, identical active counts, loss to 1e-9 relative.
+"""
+import numpy as np
+import pytest
+
+from gpu_common import max_abs, tiny
+from kb2e_amd import data
+from kb2e_amd.engine import Engine
+from oracle import orc
+from oracle.parallel import transe_parallel_batches
+
+pytestmark = pytest.mark.gpu
+
+P_ATOL = 1e-11
+
+
+def _transe_vs_model(ds, dim, epochs, *, distance=0, method=1, batches=20, rate=0.01, seed=3, apply_long=None,
+                     monkeypatch=None):
+    if apply_long is not None:
+        monkeypatch.setenv("KB2E_APPLY_LONG", str(apply_long))
+    m = orc.Model("E", dim, ds.num_entities, ds.num_relations, rate=rate, method=method, distance=distance,
+                  batches=batches)
+    m.set_triples(ds.train)
+    orc.srand(seed)
+    m.prep_train()
+    pe, pr, _ = m.tables()
+    eng = Engine("E", dim, ds.num_entities, ds.num_relations, rate=rate, method=method, distance=distance,
+                 batches=batches, seed=seed, schedule="parallel")
+    eng.upload_triples(ds.train)
+    e0, r0, _ = eng.init_params()
+    assert np.array_equal(e0, pe) and np.array_equal(r0, pr)
+    B = m.batch_size()
+    for ep in range(epochs):
+        si, sj, side = m.sample_stream(B * batches)
+        lo, ao = transe_parallel_batches(pe, pr, ds.train, si, sj, side, B, batches, rate=rate, l1=distance == 0)
+        lg, ag = eng.train_epoch()
+        assert ag == ao, (ep, ag, ao)
+        assert abs(lg - lo) <= 1e-9 * max(1.0, abs(lo))
+        ge, gr, _ = eng.download_params()
+        assert max_abs(ge, pe) < P_ATOL and max_abs(gr, pr) < P_ATOL, (ep, max_abs(ge, pe), max_abs(gr, pr))
+    return eng
+
+
+@pytest.mark.parametrize("dim,distance", [(50, 0), (100, 0), (100, 1), (17, 0), (200, 0), (130, 1)])
+def test_transe_parallel_small(dim, distance):
+    """Ragged and multi-chunk row widths on a 30k-triple set, 2 epochs."""
+    _transe_vs_model(data.synthetic("small", seed=1), dim, 2, distance=distance)
+
+
+@pytest.mark.parametrize("apply_long", [0, 1, 64])
+def test_transe_parallel_long_segments(apply_long, monkeypatch):
+    """Every segment through the 16-wave long path (1), none (0), the default split."""
+    _transe_vs_model(data.synthetic("small", seed=2), 64, 2, batches=5, apply_long=apply_long,
+                     monkeypatch=monkeypatch)
+
+
+def test_transe_parallel_single_batch_self_loops():
+    ds = data.synthetic("tiny", seed=5)
+    extra = np.array([[3, 3, 1], [7, 7, 2]] + ds.train[:50].tolist(), dtype=np.int32)
+    ds.train = np.concatenate([ds.train, extra])
+    _transe_vs_model(ds, 20, 3, batches=1, method=0)
+
+
+def test_transe_parallel_deterministic():
+    ds = data.synthetic("small", seed=4)
+    outs = []
+    for _ in range(2):
+        eng = Engine("E", 100, ds.num_entities, ds.num_relations, rate=0.01, batches=10, seed=8, schedule="parallel")
+        eng.upload_triples(ds.train)
+        eng.init_params()
+        eng.train_epoch()
+        outs.append(eng.download_params()[:2])
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+def _transr_vs_model(ds, dim, epochs, monkeypatch, *, St=8, compat=False, distance=0, batches=10, rate=0.01,
+                     seed=3, atol=1e-9):
+    from oracle.parallel import transr_parallel_batches
+    monkeypatch.setenv("KB2E_RPAR_ST", str(St))
+    m = orc.Model("R", dim, ds.num_entities, ds.num_relations, rate=rate, distance=distance, batches=batches,
+                  transr_compat=compat)
+    m.set_triples(ds.train)
+    orc.srand(seed)
+    m.prep_train()
+    pe, pr, pw = m.tables()
+    eng = Engine("R", dim, ds.num_entities, ds.num_relations, rate=rate, distance=distance, batches=batches,
+                 seed=seed, schedule="parallel", transr_compat=compat)
+    eng.upload_triples(ds.train)
+    e0, r0, w0 = eng.init_params()
+    assert np.array_equal(e0, pe) and np.array_equal(r0, pr) and np.array_equal(w0, pw)
+    eng.transr_seed(e0, r0)  # TransR seed step with the init tables (transr/trainer.cpp:88-113)
+    pe = pe / np.linalg.norm(pe, axis=1, keepdims=True)
+    work = [np.zeros(dim), np.zeros(dim)]
+    B = m.batch_size()
+    for ep in range(epochs):
+        si, sj, side = m.sample_stream(B * batches)
+        lo, ao = transr_parallel_batches(pe, pr, pw, ds.train, si, sj, side, B, batches, rate=rate,
+                                         l1=distance == 0, compat=compat, work=work, St=St)
+        lg, ag = eng.train_epoch()
+        assert ag == ao, (ep, ag, ao)
+        assert abs(lg - lo) <= 1e-9 * max(1.0, abs(lo))
+        ge, gr, gw = eng.download_params()
+        errs = (max_abs(ge, pe), max_abs(gr, pr), max_abs(gw, pw))
+        assert max(errs) < atol, (ep, errs)
+
+
+@pytest.mark.parametrize("dim,distance,St", [(20, 0, 8), (20, 1, 4), (50, 0, 8), (33, 0, 2), (20, 0, 32)])
+def test_transr_parallel_fixed(dim, distance, St, monkeypatch):
+    """Fixed (zeroed) energy; tiles of St samples (several per hot relation).  St must
+    not exceed the engine's own LDS-bounded choice (KB2E_RPAR_ST only lowers it)."""
+    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, distance=distance)
+
+
+def test_transr_parallel_compat(monkeypatch):
+    """The reference's accumulating work-vector energy (transr/transr.cpp:20-25)."""
+    _transr_vs_model(tiny(), 20, 2, monkeypatch, St=8, compat=True)
