@@ -35,6 +35,7 @@
 #include "kernels_eval.hpp"
 #include "kernels_parallel.hpp"
 #include "kernels_transr_parallel.hpp"
+#include "kernels_transr_mfma.hpp"
 
 using namespace kb2e;
 
@@ -164,8 +165,9 @@ struct kb2e_ctx {
     // PARALLEL TransR (kernels_transr_parallel.hpp)
     int32_t rpar_St = 8, rpar_max_tiles = 1;
     bool rpar_no_constraint = false;
+    bool rpar_mfma = false;  // matrix-core tile kernels (kernels_transr_mfma.hpp)
     DevBuf rpar_y, rpar_wpart, rpar_rpart, rpar_tile_act, rpar_pair, rpar_relpair, rpar_relpair_stamp, rpar_tiles,
-        rpar_ntiles, rpar_tile_first, rpar_rel_begin;
+        rpar_ntiles, rpar_tile_first, rpar_rel_begin, rpar_scan;
     hipStream_t fold_stream = nullptr;  // the long-segment fold runs beside the per-row fold
     hipEvent_t ev_fold_a = nullptr, ev_fold_b = nullptr;
     DevBuf long_list, long_count;
@@ -1290,6 +1292,18 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
             HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_long_prof), fp[1], sizeof(fp[1])));
         }
 #endif
+        if (getenv("KB2E_RPAR_STATS")) {  // transRNorm rounds of the PARALLEL TransR schedule
+            unsigned long long st[8];
+            HIPCHK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_rpar_rounds), sizeof(st)));
+            fprintf(stderr,
+                    "rpar_rounds max-per-tile sum %llu tiles %llu max %llu cycles/tile setup %.0f rounds %.0f (gemm1 %.0f "
+                    "-- %.0f) final %.0f\n",
+                    st[0], st[1], st[2], (double)st[3] / std::max(1ull, st[1]), (double)st[4] / std::max(1ull, st[1]),
+                    (double)st[6] / std::max(1ull, st[1]), (double)st[7] / std::max(1ull, st[1]),
+                    (double)st[5] / std::max(1ull, st[1]));
+            std::memset(st, 0, sizeof(st));
+            HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_rpar_rounds), st, sizeof(st)));
+        }
         if (loss) *loss = c->acc_loss;
         if (active) *active = c->acc_active;
         c->acc_loss = 0;

@@ -1,0 +1,467 @@
+// kernels_transr_mfma.hpp -- the PARALLEL TransR tile and transRNorm kernels on
+// the matrix cores (v_mfma_f64_16x16x4_f64 / v_mfma_f32_16x16x4_f32).
+//
+// Same arithmetic contract as kernels_transr_parallel.hpp (whose VALU kernels
+// remain the path when the LDS image below does not fit), recast as the dense
+// contractions they are:
+//   projections   P = V W          V: the tile's h, t, h', t' rows   (4 St x n) . (n x n)
+//   directions    Y = X W^T        X: the updates' x rows            (2 St x n) . (n x n)
+//   matrix step   dW = D^T X       D: -lr beta (h - t) rows          (n x 2 St) . (2 St x n)
+//   transRNorm    Pm = A W, A -= lr (2 Pm) W^T, dW = (-lr A0)^T G  per Jacobi round over the tile's pairs
+// Matrices live in LDS padded to NP = 16 ceil(n / 16) columns (zeros), row
+// stride L = NP + 2 (bank spread).  MFMA fragment maps (cdna_hip_programming.md
+// "Fragment layout"): A[i = l & 15][k = l >> 4], B[k = l >> 4][j = l & 15];
+// D col = l & 15, row = (l >> 4) + 4 r for f64 and 4 (l >> 4) + r for f32.
+#pragma once
+
+#include "kernels_transr_parallel.hpp"
+
+namespace kb2e {
+
+template <typename T>
+struct Mfma16;
+
+template <>
+struct Mfma16<double> {
+    typedef double acc_t __attribute__((ext_vector_type(4)));
+    static __device__ __forceinline__ acc_t mma(double a, double b, acc_t c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ int row(int l, int r) { return (l >> 4) + 4 * r; }
+};
+
+template <>
+struct Mfma16<float> {
+    typedef float acc_t __attribute__((ext_vector_type(4)));
+    static __device__ __forceinline__ acc_t mma(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ int row(int l, int r) { return 4 * (l >> 4) + r; }
+};
+
+// C = A B over 16 x 16 output tiles (MT x NT of them) and K (multiple of 4),
+// tiles dealt to the waves of the block; put(m, n, v) receives every element.
+// The fragments of eight k-steps are read from LDS before their MFMAs issue,
+// so the LDS latency is paid once per eight steps, not once per step.
+template <typename T, class FA, class FB, class FP>
+__device__ __forceinline__ void block_gemm(int MT, int NT, int K, FA A, FB B, FP put) {
+    using M = Mfma16<T>;
+    const int l = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int idx = w; idx < MT * NT; idx += nw) {
+        const int mb = idx / NT, nb = idx % NT;
+        typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
+        const int ar = mb * 16 + (l & 15), bc = nb * 16 + (l & 15), kq = l >> 4;
+        for (int kb = 0; kb < K; kb += 32) {
+            T av[8], bv[8];
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const int k = kb + 4 * s + kq;
+                const bool ok = kb + 4 * s < K;  // past K: zero operands add nothing
+                av[s] = ok ? A(ar, k) : T(0);
+                bv[s] = ok ? B(k, bc) : T(0);
+            }
+#pragma unroll
+            for (int s = 0; s < 8; ++s) acc = M::mma(av[s], bv[s], acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) put(mb * 16 + M::row(l, r), bc, acc[r]);
+    }
+}
+
+__host__ __device__ constexpr int rm_np(int n) { return (n + 15) & ~15; }
+__host__ __device__ constexpr int rm_ld(int n) { return rm_np(n) + 2; }
+__host__ __device__ constexpr int rm_up16(int v) { return (v + 15) & ~15; }
+
+// Tile kernel LDS (elements of T): W [NP][L] | V [MV][L] | P [MV][L] | X [UY][L] | D [UY][L] | coef [UY] |
+// int ids [MV], kk [St]
+template <typename T>
+__host__ __device__ constexpr size_t rmfma_tile_lds(int n, int St) {
+    return sizeof(T) * ((size_t)rm_np(n) * rm_ld(n) + 2 * (size_t)rm_up16(4 * St) * rm_ld(n) +
+                        2 * (size_t)rm_up16(2 * St) * rm_ld(n) + rm_up16(2 * St)) +
+           sizeof(int) * ((size_t)rm_up16(4 * St) + St);
+}
+
+// transRNorm kernel LDS: W [NP][L] | WT [NP][L] | A [PP][L] | G [PP][L] | Pm [PP][L] | s0 [PP] |
+// int ent_of [PP], live [PP] | counter | kk [St], act [St]
+template <typename T>
+__host__ __device__ constexpr size_t rmfma_cons_lds(int n, int St) {
+    return sizeof(T) * (2 * (size_t)rm_np(n) * rm_ld(n) + 3 * (size_t)rm_up16(4 * St + 1) * rm_ld(n) +
+                        rm_up16(4 * St + 1)) +
+           sizeof(int) * (2 * (size_t)rm_up16(4 * St + 1) + 4 + 2 * (size_t)St);
+}
+
+template <typename T>
+__device__ __forceinline__ void stage_matrix_padded(T* Wl, const T* Wg, int n, int ld) {
+    const int NP = rm_np(n), L = rm_ld(n);
+#pragma unroll 8
+    for (int idx = threadIdx.x; idx < NP * L; idx += blockDim.x) {
+        const int j = idx / L, i = idx % L;
+        Wl[idx] = (j < n && i < n) ? Wg[(int64_t)j * ld + i] : T(0);
+    }
+}
+
+// rows[row][0..L) = table row ids[row] (zeros past n, or for ids < 0), every
+// thread of the block issuing independent loads (no per-row dependent chains).
+template <typename T>
+__device__ __forceinline__ void gather_rows(T* rows, const int* ids, int nrows, const T* table, int n, int ld) {
+    const int L = rm_ld(n);
+#pragma unroll 8
+    for (int idx = threadIdx.x; idx < nrows * L; idx += blockDim.x) {
+        const int row = idx / L, i = idx % L;
+        const int e = ids[row];
+        rows[idx] = (e >= 0 && i < n) ? table[(int64_t)e * ld + i] : T(0);
+    }
+}
+
+// y_j = sum_i W[j][i] x_i from the transposed image (lane l: j = 2l, 2l+1; LDS
+// reads contiguous across lanes, x as broadcasts).
+template <typename T>
+__device__ __forceinline__ void matvec_t(const T* WT, int L, int n, const T* xl, T (&y)[2]) {
+    const int j = 2 * lane_id();
+    y[0] = y[1] = T(0);
+    if (j >= n) return;
+    T s[4][2] = {};  // four interleaved partial sums: independent LDS reads in flight
+    int i = 0;
+    for (; i + 4 <= n; i += 4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const T xi = xl[i + q];
+            s[q][0] += WT[(i + q) * L + j] * xi;
+            s[q][1] += WT[(i + q) * L + j + 1] * xi;
+        }
+    }
+    for (; i < n; ++i) {
+        const T xi = xl[i];
+        s[0][0] += WT[i * L + j] * xi;
+        s[0][1] += WT[i * L + j + 1] * xi;
+    }
+    y[0] = (s[0][0] + s[1][0]) + (s[2][0] + s[3][0]);
+    y[1] = (s[0][1] + s[1][1]) + (s[2][1] + s[3][1]);
+}
+
+// Tile: phase A (projections, energies / compat projections, x, d, y = W x) and
+// the gradient partials dW = D^T X, dr, as transr_tile_kernel.
+template <typename T, bool PROJ, bool GRAD>
+__global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParBufs<T> bf) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int t = a.tile_first[a.batch_seg[a.batch]] + blockIdx.x;
+    if (t >= a.tile_first[a.batch_seg[a.batch + 1]]) return;
+    int r, e0, cnt;
+    tile_range(a, t, r, e0, cnt);
+    const int n = a.n, ld = a.ld, NP = rm_np(n), L = rm_ld(n);
+    const int MV = rm_up16(4 * a.St), UY = rm_up16(2 * a.St);
+    T* Wl = (T*)smem;
+    T* V = Wl + NP * L;
+    T* P = V + MV * L;
+    T* X = P + MV * L;
+    T* D = X + UY * L;
+    T* coef = D + UY * L;
+    int* ids = (int*)(coef + UY);  // entity of every V row
+    int* kks = ids + MV;           // sample index of every tile sample
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = lane_id();
+    // samples of the tile: ids resolved by one thread each, then the rows gathered by all
+    for (int row = threadIdx.x; row < MV; row += blockDim.x) {
+        const int q = row >> 2, which = row & 3;
+        int e = -1;
+        if (q < cnt) {
+            const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
+            if (which == 0) kks[q] = kk;
+            const int i0 = a.si[kk], jj = a.sj[kk];
+            const int h = a.heads[i0], tt = a.tails[i0];
+            e = which == 0 ? h : which == 1 ? tt : which == 2 ? (a.side[kk] ? h : jj) : (a.side[kk] ? jj : tt);
+        }
+        ids[row] = e;
+    }
+    if (PROJ) stage_matrix_padded(Wl, bf.W + (int64_t)r * n * ld, n, ld);
+    for (int idx = threadIdx.x; idx < UY * L; idx += blockDim.x) {
+        X[idx] = T(0);
+        D[idx] = T(0);
+    }
+    for (int idx = threadIdx.x; idx < UY; idx += blockDim.x) coef[idx] = T(0);
+    __syncthreads();
+    if (PROJ) {  // V rows 4q + {0,1,2,3} = h, t, h', t' of sample q (zeros past the data)
+        gather_rows(V, ids, MV, bf.ent, n, ld);
+    }
+    __syncthreads();
+    if (PROJ) {
+        block_gemm<T>(MV / 16, NP / 16, NP, [&](int m, int k) { return V[m * L + k]; },
+                      [&](int k, int c) { return Wl[k * L + c]; }, [&](int m, int c, T v) { P[m * L + c] = v; });
+        __syncthreads();
+        // one wave per sample: energies, hinge, x, d (transr/trainer.cpp:147-164, transr/transr.cpp:26-35)
+        for (int q = w; q < cnt; q += nw) {
+            const int kk = kks[q];
+            const T* ph = P + (4 * q + 0) * L;
+            const T* pt = P + (4 * q + 1) * L;
+            const T* pnh = P + (4 * q + 2) * L;
+            const T* pnt = P + (4 * q + 3) * L;
+            T vr[2];
+            lane_pair_load(bf.rel + (int64_t)r * ld, n, vr);
+            T ep = T(0), en = T(0), xp[2], xn[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int i = 2 * l + k;
+                const bool ok = i < n;
+                const T dp = ok ? pt[i] - ph[i] - vr[k] : T(0);
+                const T dn = ok ? pnt[i] - pnh[i] - vr[k] : T(0);
+                ep += a.l1 ? fabs(dp) : dp * dp;
+                en += a.l1 ? fabs(dn) : dn * dn;
+                xp[k] = ok ? (a.l1 ? (dp > T(0) ? T(1) : T(-1)) : T(2) * dp) : T(0);
+                xn[k] = ok ? (a.l1 ? (dn > T(0) ? T(1) : T(-1)) : T(2) * dn) : T(0);
+            }
+            T dpos[2], dneg[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int i = 2 * l + k;
+                dpos[k] = i < n ? V[(4 * q + 0) * L + i] - V[(4 * q + 1) * L + i] : T(0);
+                dneg[k] = i < n ? V[(4 * q + 2) * L + i] - V[(4 * q + 3) * L + i] : T(0);
+            }
+            lane_pair_store(bf.x + ((int64_t)kk * 2 + 0) * ld, n, xp);
+            lane_pair_store(bf.x + ((int64_t)kk * 2 + 1) * ld, n, xn);
+            lane_pair_store(bf.d + ((int64_t)kk * 2 + 0) * ld, n, dpos);
+            lane_pair_store(bf.d + ((int64_t)kk * 2 + 1) * ld, n, dneg);
+            lane_pair_store(X + (2 * q + 0) * L, n, xp);
+            lane_pair_store(X + (2 * q + 1) * L, n, xn);
+            if (a.compat) {
+                double* pr = a.proj + (int64_t)kk * 4 * ld;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int i = 2 * l + k;
+                    if (i >= n) continue;
+                    pr[i] = (double)ph[i];
+                    pr[ld + i] = (double)pt[i];
+                    pr[2 * ld + i] = (double)pnh[i];
+                    pr[3 * ld + i] = (double)pnt[i];
+                }
+            } else {
+                ep = wave_sum(ep);
+                en = wave_sum(en);
+                const bool active = (double)ep + a.margin > (double)en;
+                if (l == 0) {
+                    a.act[kk] = active ? 1 : 0;
+                    a.loss[kk] = active ? a.margin + (double)ep - (double)en : 0.0;
+                }
+                if (GRAD) {
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const T c = active ? (T)(-(u ? 1.0 : -1.0) * a.lr) : T(0);  // -lr beta
+                        const T* dv = u ? dneg : dpos;
+                        const T dsc[2] = {c * dv[0], c * dv[1]};
+                        lane_pair_store(D + (2 * q + u) * L, n, dsc);
+                        if (l == 0) coef[2 * q + u] = c;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // y = W x for every update (transr/trainer.cpp:168-169): Y = X W^T
+        block_gemm<T>(UY / 16, NP / 16, NP, [&](int m, int k) { return X[m * L + k]; },
+                      [&](int k, int c) { return Wl[c * L + k]; }, [&](int m, int c, T v) {
+                          if (m < 2 * cnt && c < n) bf.y[((int64_t)kks[m >> 1] * 2 + (m & 1)) * ld + c] = v;
+                      });
+    }
+    if (!GRAD) return;
+    if (!PROJ) {  // compat: directions from phase A, hinge from the work-vector scan
+        for (int q = w; q < cnt; q += nw) {
+            const int kk = kks[q];
+            const bool act = a.act[kk] != 0;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const T c = act ? (T)(-(u ? 1.0 : -1.0) * a.lr) : T(0);
+                T xv[2], dv[2];
+                lane_pair_load(bf.x + ((int64_t)kk * 2 + u) * ld, n, xv);
+                lane_pair_load(bf.d + ((int64_t)kk * 2 + u) * ld, n, dv);
+                dv[0] *= c;
+                dv[1] *= c;
+                lane_pair_store(X + (2 * q + u) * L, n, xv);
+                lane_pair_store(D + (2 * q + u) * L, n, dv);
+                if (l == 0) coef[2 * q + u] = c;
+            }
+        }
+    }
+    __syncthreads();
+    // dW[j][i] = sum_u D[u][j] X[u][i]  (transr/trainer.cpp:166-167), this tile's partial
+    T* wp = bf.wpart + (int64_t)blockIdx.x * n * ld;
+    block_gemm<T>(NP / 16, NP / 16, UY, [&](int j, int u) { return D[u * L + j]; },
+                  [&](int u, int i) { return X[u * L + i]; }, [&](int j, int i, T v) {
+                      if (j < n && i < n) wp[(int64_t)j * ld + i] = v;
+                  });
+    if (w == 0) {  // dr = sum_u (-lr beta) x_u
+        T acc[2] = {T(0), T(0)};
+        for (int u = 0; u < 2 * cnt; ++u) {
+            const T c = coef[u];
+            acc[0] += c * X[u * L + 2 * l];
+            acc[1] += c * X[u * L + 2 * l + 1];
+        }
+        lane_pair_store(bf.rpart + (int64_t)blockIdx.x * ld, n, acc);
+        if (l == 0) {
+            int nact = 0;
+            for (int u = 0; u < 2 * cnt; ++u) nact += coef[u] != T(0);
+            a.tile_act[t] = nact;
+        }
+    }
+}
+
+// transRNorm per tile on the matrix cores, pairs and rules of
+// transr_constraint_kernel; all pairs of the tile advance together, a Jacobi
+// round per loop trip, until none violates.
+// transRNorm statistics (tools): rounds summed over tiles, tiles, most rounds in a tile
+__device__ unsigned long long g_rpar_rounds[8];  // + [3..6]: cycles per phase summed over tiles
+
+template <typename T>
+__global__ __launch_bounds__(512) void transr_constraint_mfma_kernel(RParArgs a, RParBufs<T> bf) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int t = a.tile_first[a.batch_seg[a.batch]] + blockIdx.x;
+    if (t >= a.tile_first[a.batch_seg[a.batch + 1]]) return;
+    int r, e0, cnt;
+    tile_range(a, t, r, e0, cnt);
+    const int n = a.n, ld = a.ld, NP = rm_np(n), L = rm_ld(n);
+    const int PP = rm_up16(4 * a.St + 1);
+    T* Wl = (T*)smem;
+    T* WT = Wl + NP * L;  // W transposed: lane-contiguous rows for W x
+    T* A = WT + NP * L;
+    T* G = A + PP * L;
+    T* Pm = G + PP * L;
+    T* s0 = Pm + PP * L;
+    int* ent_of = (int*)(s0 + PP);
+    int* live = ent_of + PP;
+    int* nactive = live + PP;
+    int* kks = nactive + 4;  // sample index of every tile sample
+    int* acts = kks + a.St;  // its hinge flag
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = lane_id();
+    const unsigned long long t_start = clock64();
+    const RTile tl = a.tiles[t];
+    bool relpair = false;
+    if (tl.q == 0) {
+        int any = 0;
+        for (int q = a.tile_first[tl.seg]; q < a.tile_first[tl.seg + 1]; ++q) any |= a.tile_act[q];
+        relpair = any != 0 && r < a.ne;
+    }
+    const int npairs = 4 * cnt + (relpair ? 1 : 0);
+    for (int pq = threadIdx.x; pq < PP; pq += blockDim.x) {
+        int ent = -1;
+        if (pq < 4 * cnt) {
+            const int q = pq >> 2, u = (pq >> 1) & 1, role = pq & 1;
+            const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
+            const int ac = a.act[kk];
+            if ((pq & 3) == 0) {
+                kks[q] = kk;
+                acts[q] = ac;
+            }
+            if (ac) {
+                const int i0 = a.si[kk], jj = a.sj[kk];
+                const int h = a.heads[i0], tt = a.tails[i0];
+                const int hh = u ? (a.side[kk] ? h : jj) : h;
+                const int th = u ? (a.side[kk] ? jj : tt) : tt;
+                ent = role ? th : hh;
+            }
+        } else if (pq < npairs) {
+            ent = r;  // entityVec_next_[relation] (transr/trainer.cpp:187)
+        }
+        ent_of[pq] = ent;
+    }
+    stage_matrix_padded(Wl, bf.W + (int64_t)r * n * ld, n, ld);
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < NP * L; idx += blockDim.x) {
+        const int j = idx / L, i = idx % L;
+        WT[idx] = (j < NP && i < NP) ? Wl[i * L + j] : T(0);
+    }
+    for (int pq = threadIdx.x; pq < PP; pq += blockDim.x) {  // first occurrence of each entity in the tile
+        const int ent = ent_of[pq];
+        bool lv = ent >= 0;
+        for (int k = 0; lv && k < pq; ++k) lv = ent_of[k] != ent;
+        live[pq] = lv ? ent : -1;  // the row's entity, or -1
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < PP * L; idx += blockDim.x) G[idx] = T(0);
+    gather_rows(A, live, PP, bf.ent, n, ld);
+    __syncthreads();
+    for (int row = w; row < PP; row += nw) {
+        T ss = T(0);
+        for (int i = l; i < L; i += kWave) ss += A[row * L + i] * A[row * L + i];
+        ss = wave_sum(ss);
+        if (l == 0) s0[row] = ss;
+    }
+    __syncthreads();
+    const unsigned long long t_setup = clock64();
+    const T lr = (T)a.lr;
+    // p0 = W^T a0 for every pair at once (matrix cores)
+    block_gemm<T>(PP / 16, NP / 16, NP, [&](int m, int k) { return A[m * L + k]; },
+                  [&](int k, int c) { return Wl[k * L + c]; }, [&](int m, int c, T v) { Pm[m * L + c] = v; });
+    __syncthreads();
+    const unsigned long long t_g1 = clock64();
+    // Per violating pair, one wave runs the Jacobi rounds on the projection:
+    //   p_{m+1} = p_m - 2 lr W^T (W p_m) - 2 lr (a0.a0) p_m,   G += 2 p_m,
+    // equal to re-projecting a_{m+1} = a_m - lr W g_m under the shrunk W (first
+    // order in lr); then da = -lr W G.  No block barrier inside the rounds.
+    int rounds = 0;
+    for (int row = w; row < PP; row += nw) {
+        const bool lv = live[row] >= 0;
+        T p[2], g2[2] = {T(0), T(0)};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int i = 2 * l + k;
+            p[k] = (lv && i < n) ? Pm[row * L + i] : T(0);
+        }
+        T* vrow = Pm + row * L;  // this row's scratch: p broadcast, then W p
+        int m = 0;
+        for (; lv && m < kRParMaxIter; ++m) {
+            const T xx = wave_sum(p[0] * p[0] + p[1] * p[1]);
+            if (!(xx > T(1))) break;
+            g2[0] += T(2) * p[0];
+            g2[1] += T(2) * p[1];
+            lane_pair_store(vrow, n, p);
+            wave_lds_sync();
+            T v[2];
+            matvec_t(WT, L, n, vrow, v);  // v = W p
+            wave_lds_sync();
+            lane_pair_store(vrow, n, v);
+            wave_lds_sync();
+            T q[2];  // q = W^T v: the same product on the untransposed image
+            matvec_t(Wl, L, n, vrow, q);
+            wave_lds_sync();
+            const T c = T(2) * lr * s0[row];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) p[k] = 2 * l + k < n ? p[k] - T(2) * lr * q[k] - c * p[k] : T(0);
+        }
+        rounds = max(rounds, m);
+        lane_pair_store(G + row * L, n, g2);  // G = sum of g_m (zero if the pair never violated)
+        if (l == 0) live[row] = m > 0 ? 1 : 0;  // from here on: the pair moved
+    }
+    __syncthreads();
+    const unsigned long long t_rounds = clock64();
+    if (threadIdx.x == 0) {
+        atomicAdd(&g_rpar_rounds[3], t_setup - t_start);
+        atomicAdd(&g_rpar_rounds[4], t_rounds - t_setup);
+        atomicAdd(&g_rpar_rounds[6], t_g1 - t_setup);
+        atomicAdd(&g_rpar_rounds[0], (unsigned long long)rounds);
+        atomicAdd(&g_rpar_rounds[1], 1ull);
+        atomicMax(&g_rpar_rounds[2], (unsigned long long)rounds);
+    }
+    // pair records: da = -lr W G; the matrix step uses -lr a0 (A still holds a0)
+    for (int row = w; row < PP; row += nw) {
+        T da[2] = {T(0), T(0)};
+        if (live[row]) {
+            matvec_t(WT, L, n, G + row * L, da);
+            da[0] *= -lr;
+            da[1] *= -lr;
+        }
+        if (row < 4 * cnt) {
+            const int q = row >> 2, u = (row >> 1) & 1, role = row & 1;
+            if (acts[q]) lane_pair_store(bf.pair + (((int64_t)kks[q] * 2 + u) * 2 + role) * ld, n, da);
+        } else if (row < npairs) {
+            lane_pair_store(bf.relpair + (int64_t)r * ld, n, da);
+            if (l == 0) bf.relpair_stamp[r] = bf.stamp;
+        }
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < PP * L; idx += blockDim.x) A[idx] *= -lr;
+    __syncthreads();
+    T* wp = bf.wpart + (int64_t)blockIdx.x * n * ld;
+    block_gemm<T>(NP / 16, NP / 16, PP, [&](int j, int p) { return A[p * L + j]; },
+                  [&](int p, int i) { return G[p * L + i]; }, [&](int j, int i, T v) {
+                      if (j < n && i < n) wp[(int64_t)j * ld + i] = v;
+                  });
+    if (threadIdx.x == 0) atomicAdd(&g_rpar_rounds[5], clock64() - t_rounds);
+}
+
+}  // namespace kb2e

@@ -339,12 +339,19 @@ __global__ __launch_bounds__(256) void transr_rel_rows_kernel(RParArgs a, RParBu
     T v[2];
     lane_pair_load(row, n, v);
     const int tb = a.tile_first[a.batch_seg[a.batch]];  // partials are indexed by tile within the batch
-    for (int t = t0; t < t1; ++t) {
-        T p[2];
-        const int64_t lt = t - tb;
-        lane_pair_load(j < n ? bf.wpart + (lt * n + j) * ld : bf.rpart + lt * ld, n, p);
-        v[0] += p[0];
-        v[1] += p[1];
+    for (int t = t0; t < t1; t += 4) {  // four partial rows in flight, summed in tile order
+        T p[4][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t lt = t + q - tb;
+            if (t + q < t1) lane_pair_load(j < n ? bf.wpart + (lt * n + j) * ld : bf.rpart + lt * ld, n, p[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (t + q < t1) {
+                v[0] += p[q][0];
+                v[1] += p[q][1];
+            }
     }
     if (NORM) {
         const T len = sqrt(wave_sum(v[0] * v[0] + v[1] * v[1]));
@@ -414,42 +421,52 @@ __global__ __launch_bounds__(256) void transr_constraint_kernel(RParArgs a, RPar
         const int ent = ent_of[pq];
         bool live = ent >= 0;
         for (int k = 0; live && k < pq; ++k) live = ent_of[k] != ent;  // first occurrence only
-        T a0[2] = {T(0), T(0)}, av[2], G[2] = {T(0), T(0)};
+        T a0[2] = {T(0), T(0)}, G[2] = {T(0), T(0)}, da[2] = {T(0), T(0)};
         if (live) {
             lane_pair_load(bf.ent + (int64_t)ent * ld, n, a0);
-            av[0] = a0[0];
-            av[1] = a0[1];
             const T s0 = wave_sum(a0[0] * a0[0] + a0[1] * a0[1]);
+            lane_pair_store(v4, n, a0);
+            wave_lds_sync();
+            T p[2] = {T(0), T(0)};  // p = W'^T a0
+            if (i < n)
+                for (int j = 0; j < n; ++j) {
+                    const T aj = v4[j];
+                    p[0] += Wl[j * ld + i] * aj;
+                    p[1] += Wl[j * ld + i + 1] * aj;
+                }
+            if (i + 1 >= n) p[1] = T(0);
+            if (i >= n) p[0] = T(0);
+            wave_lds_sync();
             for (int m = 0; m < kRParMaxIter; ++m) {
-                lane_pair_store(v4, n, av);
-                wave_lds_sync();
-                T p[2] = {T(0), T(0)};
-                if (i < n)
-                    for (int j = 0; j < n; ++j) {
-                        const T aj = v4[j];
-                        p[0] += Wl[j * ld + i] * aj;
-                        p[1] += Wl[j * ld + i + 1] * aj;
-                    }
-                const T ws = T(a.lr) * s0;
-                p[0] -= ws * G[0];
-                p[1] -= ws * G[1];
-                if (i + 1 >= n) p[1] = T(0);
-                if (i >= n) p[0] = T(0);
                 const T xx = wave_sum(p[0] * p[0] + p[1] * p[1]);
                 if (!(xx > T(1))) break;
-                const T g[2] = {T(2) * p[0], T(2) * p[1]};
-                G[0] += g[0];
-                G[1] += g[1];
-                lane_pair_store(v4 + ld, n, g);
+                G[0] += T(2) * p[0];
+                G[1] += T(2) * p[1];
+                lane_pair_store(v4, n, p);
                 wave_lds_sync();
-                T y[2];
-                matvec_rows(Wl, ld, n, v4 + ld, y);  // W0 g
-                av[0] -= T(a.lr) * y[0];
-                av[1] -= T(a.lr) * y[1];
+                T v[2];
+                matvec_rows(Wl, ld, n, v4, v);  // W p
+                lane_pair_store(v4 + ld, n, v);
                 wave_lds_sync();
+                T q[2] = {T(0), T(0)};  // W^T (W p)
+                if (i < n)
+                    for (int j = 0; j < n; ++j) {
+                        const T vj = v4[ld + j];
+                        q[0] += Wl[j * ld + i] * vj;
+                        q[1] += Wl[j * ld + i + 1] * vj;
+                    }
+                wave_lds_sync();
+                const T c = T(2) * T(a.lr) * s0;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) p[k] = i + k < n ? p[k] - T(2) * T(a.lr) * q[k] - c * p[k] : T(0);
             }
+            lane_pair_store(v4, n, G);
+            wave_lds_sync();
+            matvec_rows(Wl, ld, n, v4, da);  // da = -lr W G
+            da[0] *= T(-a.lr);
+            da[1] *= T(-a.lr);
+            wave_lds_sync();
         }
-        const T da[2] = {live ? av[0] - a0[0] : T(0), live ? av[1] - a0[1] : T(0)};
         if (pq < 4 * cnt) {
             const int q = pq >> 2, u = (pq >> 1) & 1, role = pq & 1;
             const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
@@ -478,36 +495,68 @@ __global__ __launch_bounds__(256) void transr_constraint_kernel(RParArgs a, RPar
 // (and the (entity[r], r) delta once), no norm.
 constexpr int kRParWaves = 16;
 
+// Events [p0 + 64 first, ...) of an entity segment in chunks of 64 (lane q:
+// event q); the rows the active ones add (y rows, or transRNorm pair deltas)
+// are then fetched four at a time, so a long segment keeps several loads in
+// flight instead of one dependent chain per event.
 template <typename T, bool GRAD>
 __device__ __forceinline__ void rpar_entity_events(const RParArgs& a, const RParBufs<T>& bf, int row, int p0, int p1,
                                                    int first, int stride, T (&acc)[2], bool& dirty, bool& er_seen) {
-    const int n = a.n, ld = a.ld;
-    for (int p = p0 + first; p < p1; p += stride) {
-        const uint64_t key = a.keys[p];
-        const int kk = a.kl.kk_of(key);
-        if (!a.act[kk]) continue;
-        const int u = (int)((key >> 3) & 1);
-        const uint32_t roles = (uint32_t)(key & 7);
-        const bool hd = roles & kRoleHead, tl = roles & kRoleTail;
-        if (GRAD) {
-            if (!hd && !tl) continue;
-            dirty = true;
-            if (hd && tl) continue;  // -beta lr y + beta lr y
-            const T c = (T)((hd ? -1.0 : 1.0) * (u ? 1.0 : -1.0) * a.lr);
-            T yv[2];
-            lane_pair_load(bf.y + ((int64_t)kk * 2 + u) * ld, n, yv);
-            acc[0] += c * yv[0];
-            acc[1] += c * yv[1];
-        } else {
-            if (roles & kRoleEntRel) er_seen = true;
+    const int n = a.n, ld = a.ld, l = lane_id();
+    for (int base = p0 + first * kWave; base < p1; base += stride * kWave) {
+        const int p = base + l;
+        int src = -1;     // row of the y / pair table this lane's event adds (GRAD: its y row)
+        int src2 = -1;    // !GRAD: second pair row (the row is head and tail of the update)
+        T c = T(0);
+        bool nrm = false, er = false;
+        if (p < p1) {
+            const uint64_t key = a.keys[p];
+            const int kk = a.kl.kk_of(key);
+            if (a.act[kk]) {
+                const int u = (int)((key >> 3) & 1);
+                const uint32_t roles = (uint32_t)(key & 7);
+                const bool hd = roles & kRoleHead, tl = roles & kRoleTail;
+                er = roles & kRoleEntRel;
+                if (GRAD) {
+                    nrm = hd || tl;
+                    if (hd != tl) {  // head and tail at once: -beta lr y + beta lr y
+                        src = kk * 2 + u;
+                        c = (T)((hd ? -1.0 : 1.0) * (u ? 1.0 : -1.0) * a.lr);
+                    }
+                } else {
+                    nrm = hd || tl;
+                    if (hd) src = (kk * 2 + u) * 2 + 0;
+                    if (tl) {
+                        if (src < 0) src = (kk * 2 + u) * 2 + 1;
+                        else src2 = (kk * 2 + u) * 2 + 1;
+                    }
+                }
+            }
+        }
+        if (__ballot(nrm)) dirty = true;
+        if (__ballot(er)) er_seen = true;
+        const T* tab = GRAD ? bf.y : bf.pair;
+        for (int pass = 0; pass < (GRAD ? 1 : 2); ++pass) {
+            const int mine = pass ? src2 : src;
+            uint64_t m = __ballot(mine >= 0);
+            while (m) {
+                int ev[4];
+                int k = 0;
+                for (; k < 4 && m; ++k) {
+                    ev[k] = __builtin_ctzll(m);
+                    m &= m - 1;
+                }
+                T v[4][2];
 #pragma unroll
-            for (int role = 0; role < 2; ++role) {
-                if (!(role ? tl : hd)) continue;
-                T dv[2];
-                lane_pair_load(bf.pair + (((int64_t)kk * 2 + u) * 2 + role) * ld, n, dv);
-                acc[0] += dv[0];
-                acc[1] += dv[1];
-                dirty = true;
+                for (int q = 0; q < 4; ++q)
+                    if (q < k) lane_pair_load(tab + (int64_t)readlane_i32(mine, ev[q]) * ld, n, v[q]);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (q < k) {
+                        const T cq = GRAD ? readlane_f(c, ev[q]) : T(1);
+                        acc[0] += cq * v[q][0];
+                        acc[1] += cq * v[q][1];
+                    }
             }
         }
     }
@@ -554,7 +603,7 @@ __global__ __launch_bounds__(1024) void transr_entity_kernel(RParArgs a, RParBuf
         __syncthreads();
         T acc[2] = {T(0), T(0)};
         bool dirty = false, er = false;
-        rpar_entity_events<T, GRAD>(a, bf, row, p0, p1, w, kRParWaves, acc, dirty, er);
+        rpar_entity_events<T, GRAD>(a, bf, row, p0, p1, w, kRParWaves, acc, dirty, er);  // chunks w, w + 16, ...
         part[w][0][l] = acc[0];
         part[w][1][l] = acc[1];
         if (l == 0 && dirty) atomicOr(&flags[0], 1);
@@ -580,6 +629,55 @@ __global__ __launch_bounds__(1024) void transr_entity_kernel(RParArgs a, RParBuf
         bool dirty = false, er = false;
         rpar_entity_events<T, GRAD>(a, bf, row, p0, p1, 0, 1, acc, dirty, er);
         rpar_entity_finish<T, GRAD>(a, bf, row, acc, dirty, er);
+    }
+}
+
+// ---- compat energy: the work-vector prefix scan over the batch's calls -------
+//
+// transr/transr.cpp:20-25 never zeroes the work vectors, so call c of the
+// batch (pos, neg of sample 0, then of sample 1, ...) sees work + the sum of
+// the projections of calls 0..c.  Three passes over chunks of kScanChunk calls
+// (chunk sums; prefix over chunks from the carried work vectors; inclusive scan
+// inside each chunk), one thread per (head/tail, element), coalesced rows.
+constexpr int kScanChunk = 64;
+
+__global__ __launch_bounds__(256) void rpar_scan_sums_kernel(const double* proj, int64_t calls, int32_t ld,
+                                                             int32_t n, double* sums) {
+    const int c = blockIdx.x;
+    const int64_t c0 = (int64_t)c * kScanChunk, c1 = min<int64_t>(calls, c0 + kScanChunk);
+    for (int e = threadIdx.x; e < 2 * n; e += blockDim.x) {
+        const int side = e / n, i = e % n;
+        double s = 0;
+        for (int64_t k = c0; k < c1; ++k) s += proj[(k * 2 + side) * ld + i];
+        sums[(int64_t)c * 2 * n + e] = s;
+    }
+}
+
+__global__ __launch_bounds__(256) void rpar_scan_prefix_kernel(double* sums, int32_t nchunks, int32_t n,
+                                                               double* work) {
+    for (int e = threadIdx.x; e < 2 * n; e += blockDim.x) {
+        double run = work[e];  // work = [head n][tail n]
+        for (int c = 0; c < nchunks; ++c) {
+            const double s = sums[(int64_t)c * 2 * n + e];
+            sums[(int64_t)c * 2 * n + e] = run;  // exclusive prefix
+            run += s;
+        }
+        work[e] = run;
+    }
+}
+
+__global__ __launch_bounds__(256) void rpar_scan_apply_kernel(double* proj, int64_t calls, int32_t ld, int32_t n,
+                                                              const double* sums) {
+    const int c = blockIdx.x;
+    const int64_t c0 = (int64_t)c * kScanChunk, c1 = min<int64_t>(calls, c0 + kScanChunk);
+    for (int e = threadIdx.x; e < 2 * n; e += blockDim.x) {
+        const int side = e / n, i = e % n;
+        double run = sums[(int64_t)c * 2 * n + e];
+        for (int64_t k = c0; k < c1; ++k) {
+            double* p = proj + (k * 2 + side) * ld + i;
+            run += *p;
+            *p = run;
+        }
     }
 }
 

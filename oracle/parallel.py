@@ -150,7 +150,9 @@ def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St, dedupe=True, relpa
     Per tile (relation, St samples in kk order): pairs (h', r), (t', r) of the
     active updates in (sample, update, role) order, then (entity'[r], r) on the
     relation's first tile; first occurrences only; the loop in Jacobi form to
-    first order (kernels_transr_parallel.hpp, transr_constraint_kernel).
+    first order, iterated on the projection p = W^T a:
+    p <- p - 2 lr W^T W p - 2 lr |a0|^2 p, G += 2 p while |p|^2 > 1, then
+    da = -lr W G, dW = -lr a0 G^T (kernels_transr_mfma.hpp).
     """
     ra = np.unique(r[act])
     W0 = W.copy()
@@ -171,16 +173,15 @@ def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St, dedupe=True, relpa
                     continue
                 seen.add(e)
                 a0 = E1[e]
-                av = a0.copy()
+                Wm = W0[rr]
                 G = np.zeros_like(a0)
                 s0 = a0 @ a0
+                p = Wm.T @ a0
                 for _ in range(max_iter):
-                    p = W0[rr].T @ av - rate * s0 * G
                     if not (p @ p > 1.0):
                         break
-                    g = 2.0 * p
-                    G += g
-                    av = av - rate * (W0[rr] @ g)
-                ent[e] += av - a0
+                    G += 2.0 * p
+                    p = p - 2.0 * rate * (Wm.T @ (Wm @ p)) - 2.0 * rate * s0 * p
+                ent[e] += -rate * (Wm @ G)
                 dWc[rr] += np.outer(-rate * a0, G)
     W[ra] += dWc[ra]
