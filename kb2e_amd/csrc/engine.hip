@@ -36,6 +36,7 @@
 #include "kernels_parallel.hpp"
 #include "kernels_transr_parallel.hpp"
 #include "kernels_transr_mfma.hpp"
+#include "kernels_transh_parallel.hpp"
 
 using namespace kb2e;
 
@@ -96,9 +97,11 @@ void check_dataflow(kb2e_ctx* c);
 void build_owner_index(kb2e_ctx* c);
 void prepare_relowner_kernels();
 void setup_transr_parallel(kb2e_ctx* c);
-void build_transr_tiles(kb2e_ctx* c);
+void build_transr_tiles(kb2e_ctx* c, bool tiles);
 template <typename T>
 void run_batch_transr_parallel(kb2e_ctx* c, int64_t b);
+template <typename T, int CH>
+void run_batch_transh_parallel(kb2e_ctx* c, int64_t b);
 }  // namespace
 
 struct kb2e_ctx {
@@ -160,6 +163,7 @@ struct kb2e_ctx {
     int32_t apply_long_min = 256;  // KB2E_APPLY_LONG: PARALLEL-schedule segments this long take a 16-wave workgroup
     int32_t par_long_cap = 1, apply_grid = 256;
     DevBuf par_long_list, par_long_count;  // per epoch: long segments of every batch
+    DevBuf hpar_orth;                      // PARALLEL TransH: orthogonality flags per sample
     // PARALLEL schedule: per-event records in sorted order (kernels_transe.hpp EventRecs)
     DevBuf ev_iota, ev_slot_sorted, ev_inv, seg_row, ev_meta, ev_words;
     // PARALLEL TransR (kernels_transr_parallel.hpp)
@@ -403,9 +407,9 @@ void build_index(kb2e_ctx* c) {
             seg_rows_kernel<<<256, 256, 0, c->stream>>>(c->keys_sorted.as<uint64_t>(), c->seg_start.as<int32_t>(),
                                                        c->nseg.as<int32_t>(), c->kl, c->seg_row.as<int32_t>());
             HIPCHK(hipGetLastError());
-            if (c->cfg.model == KB2E_TRANSR) build_transr_tiles(c);
+            if (c->cfg.model != KB2E_TRANSE) build_transr_tiles(c, c->cfg.model == KB2E_TRANSR);
         }
-        if (c->cfg.model == KB2E_TRANSE && c->cfg.schedule == KB2E_SCHEDULE_PARALLEL && c->apply_long_min > 0) {
+        if (c->cfg.model != KB2E_TRANSR && c->cfg.schedule == KB2E_SCHEDULE_PARALLEL && c->apply_long_min > 0) {
             long_lists_kernel<<<(int)c->nb, 1024, 0, c->stream>>>(
                 c->seg_start.as<int32_t>(), c->batch_seg.as<int32_t>(), c->apply_long_min, c->par_long_cap,
                 c->par_long_list.as<int32_t>(), c->par_long_count.as<int32_t>());
@@ -744,6 +748,12 @@ void run_batch(kb2e_ctx* c, int64_t b) {
         }
     } else if (c->cfg.model == KB2E_TRANSR && c->parallel()) {
         run_batch_transr_parallel<T>(c, b);
+    } else if (c->cfg.model == KB2E_TRANSH && c->parallel()) {
+        switch (c->ch) {
+            case 1: run_batch_transh_parallel<T, 1>(c, b); break;
+            case 2: run_batch_transh_parallel<T, 2>(c, b); break;
+            default: run_batch_transh_parallel<T, 4>(c, b); break;
+        }
     } else {
         run_batch_relowner<T>(c, b);
     }
@@ -939,7 +949,7 @@ void setup_epoch_buffers(kb2e_ctx* c) {
         c->xreal.alloc((size_t)c->B * 2 * c->ld * c->esize);
     c->stats.alloc((2 + 2 * kStatSlices) * 8);
     HIPCHK(hipMemset(c->stats.p, 0, c->stats.bytes));
-    if (g.model == KB2E_TRANSE && g.schedule == KB2E_SCHEDULE_PARALLEL) {
+    if (g.model != KB2E_TRANSR && g.schedule == KB2E_SCHEDULE_PARALLEL) {
         const int64_t per_batch = c->B * c->slots;
         c->par_long_cap = (int32_t)(c->apply_long_min > 0 ? std::min<int64_t>(per_batch, per_batch / c->apply_long_min + 1)
                                                          : 1);
@@ -951,6 +961,13 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     }
     setup_relowner_buffers(c);
     if (g.model == KB2E_TRANSR && g.schedule == KB2E_SCHEDULE_PARALLEL) setup_transr_parallel(c);
+    if (g.model == KB2E_TRANSH && g.schedule == KB2E_SCHEDULE_PARALLEL) {
+        c->hpar_orth.alloc((size_t)((c->B + 511) / 512) * 512);  // whole 8-byte words past B stay zero
+        HIPCHK(hipMemset(c->hpar_orth.p, 0, c->hpar_orth.bytes));
+        c->rpar_St = 1 << 30;  // build_transr_tiles(c, false): relation segment ranges only
+        c->rpar_ntiles.alloc((size_t)(nkeys + 1) * 4);
+        c->rpar_rel_begin.alloc((size_t)c->nb * 4);
+    }
     c->device_bytes = 0;
     for (DevBuf* d : {&c->ent, &c->rel, &c->w, &c->heads, &c->tails, &c->rels, &c->si_[0], &c->sj_[0], &c->side_[0],
                       &c->si_[1], &c->sj_[1], &c->side_[1], &c->filter_slots, &c->pr_dev,
@@ -963,6 +980,7 @@ void setup_epoch_buffers(kb2e_ctx* c) {
 
 #include "engine_relowner.inc"
 #include "engine_transr_parallel.inc"
+#include "engine_transh_parallel.inc"
 
 namespace {
 template <typename T, int CH>
@@ -1012,7 +1030,6 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
         (g.schedule != KB2E_SCHEDULE_ORDERED && g.schedule != KB2E_SCHEDULE_PARALLEL))
         return KB2E_EINVAL;
     if (g.model == KB2E_TRANSR && g.num_relations > g.num_entities) return KB2E_EINVAL;
-    if (g.schedule == KB2E_SCHEDULE_PARALLEL && g.model == KB2E_TRANSH) return KB2E_EUNSUPPORTED;
     if (g.schedule == KB2E_SCHEDULE_PARALLEL && g.model == KB2E_TRANSR && g.dim > 128) return KB2E_EUNSUPPORTED;  // entityVec_next_[relation]
     if (g.model == KB2E_TRANSR && ((size_t)g.dim * (g.dim + 1) + 3 * (size_t)g.dim) * (g.precision / 8) > 96 * 1024)
         return KB2E_EUNSUPPORTED;  // the owner's relation matrix must fit in LDS
@@ -1075,8 +1092,8 @@ kb2e_status kb2e_upload_triples(kb2e_ctx* c, const int32_t* h, const int32_t* t,
         if (c->cfg.method == 0) std::fill(pr.begin(), pr.end(), 500.0);  // common/trainer.cpp:84-86
         c->pr_dev.alloc(pr.size() * 8);
         HIPCHK(hipMemcpy(c->pr_dev.p, pr.data(), pr.size() * 8, hipMemcpyHostToDevice));
-        if (c->cfg.model == KB2E_TRANSR && c->parallel()) {
-            // PARALLEL TransR: every relation is its own event row (relation segments = tiles)
+        if (c->cfg.model != KB2E_TRANSE && c->parallel()) {
+            // PARALLEL TransH/TransR: every relation is its own event row
             c->plan.num_owners = c->cfg.num_relations;
             c->plan.owner.resize(c->cfg.num_relations);
             for (int r = 0; r < c->cfg.num_relations; ++r) c->plan.owner[r] = r;

@@ -34,6 +34,7 @@
 
 #include "host_data.hpp"
 #include "kernels_common.hpp"
+#include "kernels_transe.hpp"
 
 namespace kb2e {
 
@@ -206,11 +207,16 @@ struct HScoreArgs {
 };
 
 // transh/transh.cpp:10-29 energies, transh/trainer.cpp:14-33 directions.
-template <typename T, int CH>
-__global__ __launch_bounds__(256) void transh_score_kernel(HScoreArgs<T> a) {
+// EMIT (PARALLEL schedule): also the event records of the h/t/r updates, whose
+// deltas are TransE's (transh/trainer.cpp:34-37; kernels_transe.hpp EventSlot).
+template <typename T, int CH, bool EMIT = false>
+__global__ __launch_bounds__(256) void transh_score_kernel(HScoreArgs<T> a, EventRecs er = {}, KeyLayout kl = {},
+                                                           int64_t kbase = 0, int32_t ne = 0) {
     const int kk = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (kk >= a.B) return;
     const int l = lane_id();
+    EventSlot slot;
+    if (EMIT) slot.prefetch(er, kbase + kk);
     const int i = a.si[kk], j = a.sj[kk];
     const int h = a.heads[i], t = a.tails[i], r = a.rels[i];
     const int nh = a.side[kk] ? h : j, nt = a.side[kk] ? j : t;
@@ -254,7 +260,11 @@ __global__ __launch_bounds__(256) void transh_score_kernel(HScoreArgs<T> a) {
         a.act[kk] = active ? 1 : 0;
         a.loss[kk] = active ? a.margin + e_pos - e_neg : 0.0;
     }
-    if (!active) return;
+    uint64_t bpw[CH * kVec], bnw[CH * kVec];
+    if (!active) {
+        if (EMIT) slot.write<CH * kVec>(er, kl, ne, kk, false, bpw, bnw, a.nw);
+        return;
+    }
     // sum_x = sum_i x_i w_i with x_i = +-1 (transh/trainer.cpp:33)
     T sx_p = T(0), sx_n = T(0);
 #pragma unroll
@@ -274,11 +284,14 @@ __global__ __launch_bounds__(256) void transh_score_kernel(HScoreArgs<T> a) {
             const bool valid = elem_valid(c, k, a.n);
             const uint64_t bp = __ballot(valid && dp[c][k] > T(0));
             const uint64_t bn = __ballot(valid && dn[c][k] > T(0));
+            bpw[c * kVec + k] = bp;
+            bnw[c * kVec + k] = bn;
             if (l == 0) {
                 a.xbits[((int64_t)kk * 2 + 0) * a.nw + c * kVec + k] = bp;
                 a.xbits[((int64_t)kk * 2 + 1) * a.nw + c * kVec + k] = bn;
             }
         }
+    if (EMIT) slot.write<CH * kVec>(er, kl, ne, kk, true, bpw, bnw, a.nw);
     if (l == 0) {
         T* s0 = a.scal + ((int64_t)kk * 2 + 0) * 4;
         T* s1 = a.scal + ((int64_t)kk * 2 + 1) * 4;

@@ -1,0 +1,216 @@
+// kernels_transh_parallel.hpp -- TransH under the PARALLEL schedule
+// (KB2E_SCHEDULE_PARALLEL; kernels_parallel.hpp has the TransE form).
+//
+// The reference's TransH step (transh/trainer.cpp:11-59) for one update
+// (h, t, r, beta), from the snapshot: hs = w.h, ts = w.t,
+// x = sign(2((t - ts w) - (h - hs w) - r)), sum_x = x.w;
+//   r' -= beta lr x,  h' -= beta lr x,  t' += beta lr x          (the TransE deltas)
+//   w' += beta lr (hs - ts) x + beta lr sum_x (h - t)
+//   norm(r'), norm(h'), norm(t') (<= 1), norm(w', false) (unit),
+//   normOrth(r', w'), normOrth(h', w'), normOrth(t', w')       (common/utils.cpp:79-111)
+// Here: the h/t/r rows take the TransE apply (summed sign counts, one norm);
+// every relation's w gets its summed delta and one unit norm (one workgroup per
+// relation, waves over chunks of its updates); then every (row, w') pair of an
+// active update is checked (w'.a > 0.1), and the few violating pairs run the
+// reference's normOrth loop in sample order on one wave, exactly as written
+// (including its never-reset `sum`).
+#pragma once
+
+#include "kernels_relowner.hpp"
+
+namespace kb2e {
+
+template <typename T>
+struct HParArgs {
+    const int32_t* heads;
+    const int32_t* tails;
+    const int32_t* rels;
+    const int32_t* si;
+    const int32_t* sj;
+    const uint8_t* side;
+    int32_t B, n, ld, nw, ne, nr;
+    int32_t batch;
+    double lr;
+    const uint64_t* keys;
+    const int32_t* seg_start;
+    const int32_t* batch_seg;
+    const int32_t* seg_row;
+    const int32_t* rel_begin;
+    const uint8_t* act;
+    const int32_t* meta;      // event records (kernels_transe.hpp EventRecs)
+    const uint64_t* words;
+    const T* scal;            // [B][2][4] hs, ts, sum_x
+    const T* snap;            // [B][2][2][ld] snapshot head, tail rows
+    T* ent;
+    T* rel;
+    T* w;
+    uint8_t* orth_mask;       // [B] violating (update, row) pairs of each sample, bits u * 3 + {r, h, t}
+};
+
+// One 1024-thread workgroup per relation segment of the batch: waves sum
+// chunks of its events, partial sums combined in wave order, wave 0 applies.
+template <typename T, int CH>
+__global__ __launch_bounds__(1024) void transh_w_apply_kernel(HParArgs<T> a) {
+    __shared__ T part[16][CH * kVec][kWave];
+    __shared__ int any;
+    const int s = a.rel_begin[a.batch] + blockIdx.x;
+    if (s >= a.batch_seg[a.batch + 1]) return;
+    const int w = threadIdx.x >> 6, l = lane_id();
+    const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
+    const int r = a.seg_row[s] - a.ne;
+    if (threadIdx.x == 0) any = 0;
+    __syncthreads();
+    T acc[CH][kVec] = {};
+    bool act_any = false;
+    for (int base = p0 + w * kWave; base < p1; base += 16 * kWave) {
+        const int p = base + l;
+        int xrow = -1;
+        if (p < p1) {
+            const int32_t meta = a.meta[p];
+            if (((meta & 3) - 1) != 0) xrow = meta >> 4;  // active update: kk * 2 + u
+        }
+        uint64_t m = __ballot(xrow >= 0);
+        if (m) act_any = true;
+        while (m) {  // eight updates at a time: their loads in flight together
+            constexpr int G = 8;
+            int ev[G], xr[G];
+            int ne4 = 0;
+            for (; ne4 < G && m; ++ne4) {
+                ev[ne4] = __builtin_ctzll(m);
+                m &= m - 1;
+                xr[ne4] = readlane_i32(xrow, ev[ne4]);
+            }
+            T hs[G], ts[G], sx[G], hv[G][CH][kVec], tv[G][CH][kVec];
+            uint64_t words[G][2 * CH];
+#pragma unroll
+            for (int q = 0; q < G; ++q) {
+                if (q >= ne4) continue;
+                const T* sc = a.scal + (int64_t)xr[q] * 4;
+                hs[q] = sc[0];
+                ts[q] = sc[1];
+                sx[q] = sc[2];
+                const T* hrow = a.snap + ((int64_t)xr[q] * 2 + 0) * a.ld;
+                const T* trow = a.snap + ((int64_t)xr[q] * 2 + 1) * a.ld;
+#pragma unroll
+                for (int cc = 0; cc < CH; ++cc)
+#pragma unroll
+                    for (int k = 0; k < kVec; ++k) {
+                        const int el = cc * (kWave * kVec) + l * kVec + k;
+                        hv[q][cc][k] = el < a.n ? hrow[el] : T(0);
+                        tv[q][cc][k] = el < a.n ? trow[el] : T(0);
+                    }
+#pragma unroll
+                for (int wq = 0; wq < 2 * CH; ++wq)
+                    words[q][wq] = wq < a.nw ? a.words[(int64_t)(base + ev[q]) * a.nw + wq] : 0ull;
+            }
+#pragma unroll
+            for (int q = 0; q < G; ++q) {
+                if (q >= ne4) continue;
+                const T c = (T)(((xr[q] & 1) ? 1.0 : -1.0) * a.lr);  // beta lr
+#pragma unroll
+                for (int cc = 0; cc < CH; ++cc)
+#pragma unroll
+                    for (int k = 0; k < kVec; ++k) {
+                        if (!elem_valid(cc, k, a.n)) continue;
+                        const T x = xbit(words[q], cc, k) ? T(1) : T(-1);
+                        acc[cc][k] += c * ((hs[q] - ts[q]) * x + sx[q] * (hv[q][cc][k] - tv[q][cc][k]));
+                    }
+            }
+        }
+    }
+#pragma unroll
+    for (int cc = 0; cc < CH; ++cc)
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) part[w][cc * kVec + k][l] = acc[cc][k];
+    if (act_any && l == 0) atomicOr(&any, 1);
+    __syncthreads();
+    if (w != 0 || !any) return;
+    RowReg<T, CH> W;
+    T* wrow = a.w + (int64_t)r * a.ld;
+    W.load(wrow, a.n);
+#pragma unroll
+    for (int cc = 0; cc < CH; ++cc)
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            T sum = part[0][cc * kVec + k][l];
+            for (int v = 1; v < 16; ++v) sum += part[v][cc * kVec + k][l];
+            if (elem_valid(cc, k, a.n)) W.v[cc][k] = W.v[cc][k] + sum;
+        }
+    W.norm(a.n, false);
+    W.store(wrow, a.n);
+}
+
+// One wave per active sample: w'.a for the rows r', h', t' of both updates
+// (after every norm); bit set where the reference's loop would move them.
+template <typename T, int CH>
+__global__ __launch_bounds__(256) void transh_orth_check_kernel(HParArgs<T> a) {
+    const int kk = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (kk >= a.B) return;
+    const int l = lane_id();
+    if (!a.act[kk]) {
+        if (l == 0) a.orth_mask[kk] = 0;
+        return;
+    }
+    const int i0 = a.si[kk], j = a.sj[kk];
+    const int h = a.heads[i0], t = a.tails[i0], r = a.rels[i0];
+    const int nh = a.side[kk] ? h : j, nt = a.side[kk] ? j : t;
+    RowReg<T, CH> W;
+    W.load(a.w + (int64_t)r * a.ld, a.n);
+    const T* rows[6] = {a.rel + (int64_t)r * a.ld, a.ent + (int64_t)h * a.ld, a.ent + (int64_t)t * a.ld,
+                        a.rel + (int64_t)r * a.ld, a.ent + (int64_t)nh * a.ld, a.ent + (int64_t)nt * a.ld};
+    uint32_t mask = 0;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        if (q == 3) continue;  // the relation row is checked once: its second check sees the same rows
+        RowReg<T, CH> A;
+        A.load(rows[q], a.n);
+        T x = T(0);
+#pragma unroll
+        for (int cc = 0; cc < CH; ++cc)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) x += W.v[cc][k] * A.v[cc][k];
+        if (wave_sum(x) > T(0.1)) mask |= 1u << q;
+    }
+    if (l == 0) a.orth_mask[kk] = (uint8_t)mask;
+}
+
+// One wave, samples in order: the reference's normOrth (common/utils.cpp:79-111,
+// orth_norm) on every flagged pair, in place on the live rows.
+template <typename T, int CH>
+__global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
+    const int l = lane_id();
+    // eight samples' flags per lane (orth_mask is zero past B up to a multiple of 512)
+    for (int base = 0; base < a.B; base += 8 * kWave) {
+        const uint64_t word = *reinterpret_cast<const uint64_t*>(a.orth_mask + base + 8 * l);
+        uint64_t m = __ballot(word != 0ull);
+        while (m) {
+            const int e = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint64_t wd = readlane_u64(word, e);
+            for (int by = 0; by < 8; ++by) {
+                const uint32_t bits = (uint32_t)((wd >> (8 * by)) & 0xffu);
+                if (!bits) continue;
+                const int k2 = base + 8 * e + by;
+                const int i0 = a.si[k2], j = a.sj[k2];
+                const int h = a.heads[i0], t = a.tails[i0], r = a.rels[i0];
+                const int nh = a.side[k2] ? h : j, nt = a.side[k2] ? j : t;
+                T* rows[6] = {a.rel + (int64_t)r * a.ld, a.ent + (int64_t)h * a.ld, a.ent + (int64_t)t * a.ld,
+                              a.rel + (int64_t)r * a.ld, a.ent + (int64_t)nh * a.ld, a.ent + (int64_t)nt * a.ld};
+                T* wrow = a.w + (int64_t)r * a.ld;
+                for (int q = 0; q < 6; ++q) {
+                    if (!((bits >> q) & 1u)) continue;
+                    // agent-scope (L1-bypassing) accesses: a later pair may reload a row stored here
+                    RowReg<T, CH> A, W;
+                    row_load_sc1(A, rows[q], a.n);
+                    row_load_sc1(W, wrow, a.n);
+                    orth_norm<T, CH>(A, W, a.n, (T)a.lr);
+                    row_store_sc1(A, rows[q], a.n);
+                    row_store_sc1(W, wrow, a.n);
+                    drain_stores();
+                }
+            }
+        }
+    }
+}
+
+}  // namespace kb2e

@@ -140,3 +140,37 @@ def test_transr_parallel_fp32_close(monkeypatch):
         out[prec] = [eng.train_epoch() for _ in range(2)]
     for (l64, a64), (l32, a32) in zip(out[64], out[32]):
         assert abs(a64 - a32) <= 0.01 * a64 and abs(l64 - l32) <= 0.01 * l64
+
+
+def _transh_vs_model(ds, dim, epochs, *, batches=10, rate=0.01, seed=3, method=1, atol=1e-9):
+    from oracle.parallel import transh_parallel_batches
+    m = orc.Model("H", dim, ds.num_entities, ds.num_relations, rate=rate, method=method, batches=batches)
+    m.set_triples(ds.train)
+    orc.srand(seed)
+    m.prep_train()
+    pe, pr, pw = m.tables()
+    eng = Engine("H", dim, ds.num_entities, ds.num_relations, rate=rate, method=method, batches=batches, seed=seed,
+                 schedule="parallel")
+    eng.upload_triples(ds.train)
+    e0, r0, w0 = eng.init_params()
+    assert np.array_equal(e0, pe) and np.array_equal(r0, pr) and np.array_equal(w0, pw)
+    B = m.batch_size()
+    for ep in range(epochs):
+        si, sj, side = m.sample_stream(B * batches)
+        lo, ao = transh_parallel_batches(pe, pr, pw, ds.train, si, sj, side, B, batches, rate=rate)
+        lg, ag = eng.train_epoch()
+        assert ag == ao, (ep, ag, ao)
+        assert abs(lg - lo) <= 1e-9 * max(1.0, abs(lo))
+        ge, gr, gw = eng.download_params()
+        errs = (max_abs(ge, pe), max_abs(gr, pr), max_abs(gw, pw))
+        assert max(errs) < atol, (ep, errs)
+
+
+@pytest.mark.parametrize("dim", [20, 100, 17, 130])
+def test_transh_parallel(dim):
+    """Tiny set, lr 0.01: the orthogonality loop fires; ragged and multi-chunk widths."""
+    _transh_vs_model(tiny(), dim, 2)
+
+
+def test_transh_parallel_small():
+    _transh_vs_model(data.synthetic("small", seed=1), 64, 2, batches=20, rate=0.001)
