@@ -9,10 +9,18 @@ FB15k-shaped data, 14,951 entities / 1,345 relations / 483,142 triples), FP64
 like the reference.  `value` = training triples (samples) per second over the
 whole job, inputs resident in HBM; epochs' sampling + index build included.
 
-N>1 (torchrun): strong scaling -- the triple set is fixed; each rank owns the
-triples whose head hashes to it and trains its shard; at every
-epoch boundary the ranks sum their table deltas over RCCL and re-apply the norm
-constraints (kb2e_amd.distributed).
+Schedules (include/kb2e_engine.h kb2e_schedule): `value` is the PARALLEL
+schedule (the data-parallel form: the reference's sample stream, snapshot
+energies, hinge decisions and directions; summed row deltas and one norm per
+batch; link-prediction parity in DESIGN.md), and the same line carries the
+ORDERED schedule (bit-faithful to the reference) measured on the same
+workload under "schedules".
+
+N>1 (torchrun): each rank owns the triples whose head hashes to it
+ and runs batches of the single-GPU size over its shard
+(100 / N batches per epoch), so per-GPU work per step is fixed (weak scaling);
+at every epoch boundary the ranks sum their table deltas over RCCL and
+re-apply the norm constraints (kb2e_amd.distributed).
 """
 import argparse
 import json
@@ -121,6 +129,112 @@ def cpu_baseline(cfg_name, ds, budget_s=25.0):
             "sample": f"{nb} batches ({B} samples each) of the C restatement, 1 thread"}
 
 
+def phase_bytes(model, n, s, a):
+    """(phase A bytes, phase B bytes) per sample."""
+    _, score_b, fold_b = algorithmic_bytes_per_sample(model, n, s, a)
+    return score_b, fold_b
+
+
+def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup):
+    """Train `warmup` then time `steps` batches of one schedule; returns a dict."""
+    from kb2e_amd.engine import Engine
+
+    model, shape, dim, method, distance, rate = CONFIGS[args.config]
+    batches = max(1, 100 // world)
+    eng = Engine(model, dim, ds.num_entities, ds.num_relations, rate=rate, method=method, distance=distance,
+                 batches=batches, seed=7 + rank, precision=args.precision, device=local if world > 1 else 0,
+                 schedule=schedule)
+    eng.upload_triples(train)
+    ent, rel, w = eng.init_params()
+    if model == "R":
+        eng.transr_seed(ent, rel)  # seed = the init draws (no TransE run in the bench)
+    B = len(train) // batches
+    merger = None
+    if world > 1:
+        from kb2e_amd.distributed import EpochMerger
+        merger = EpochMerger(eng, dist)
+
+    def run(k_steps):
+        done = 0
+        while done < k_steps:
+            k = min(k_steps - done, batches - (run.pos % batches))
+            eng.train_batches(k)
+            done += k
+            run.pos += k
+            if merger is not None and run.pos % batches == 0:
+                merger.merge()
+    run.pos = 0
+
+    run(warmup)
+    eng.synchronize()
+    eng.take_stats()
+    # HIP-event timing of the batch kernels on every 10th batch (events cost
+    # device time; sampling keeps the timed run unperturbed)
+    eng.profile(10)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    run(steps)
+    eng.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    loss, active = eng.take_stats()
+    # phase B span: TransE/TransH "fold_phase" (ordered: per-row folds; parallel:
+    # the apply kernels), TransR "apply" (parallel) or the relation owners (ordered)
+    if model == "R":
+        fold_name = "apply" if schedule == "parallel" else "relowner"
+    elif model == "H":
+        fold_name = "fold_phase" if schedule == "parallel" else "relowner"
+    else:
+        fold_name = "apply" if schedule == "parallel" else "fold_phase"
+    fold_ms, fold_n = eng.profile_query(fold_name)
+    score_ms, score_n = eng.profile_query("score")
+    kernels_us = {}
+    for k in ("score", "fold", "fold_long", "apply", "tickets", "desc", "relowner", "fold_phase"):
+        ms, n = eng.profile_query(k)
+        if n:
+            kernels_us[k] = ms / n * 1e3
+    eng.close()
+    samples = steps * B
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed, float(samples), float(active)], dtype=torch.float64, device="cuda")
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed = float(mx[0])
+        samples = float(t[1])
+        active = float(t[2])
+    a = active / max(1.0, samples)
+    s = 8 if args.precision == 64 else 4
+    score_b, fold_b = phase_bytes(model, dim, s, a)
+    per_sample = score_b + fold_b
+    if fold_ms >= score_ms:
+        dominant, avg_ms, bytes_per_launch = fold_name, fold_ms / max(1, fold_n), fold_b * B
+    else:
+        dominant, avg_ms, bytes_per_launch = "score", score_ms / max(1, score_n), score_b * B
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}_{schedule}_f{args.precision}.json")
+    if os.path.exists(pmc):
+        try:
+            fams = json.load(open(pmc))
+            v = fams.get(dominant, {}).get("hbm_bytes_per_launch")
+            traffic = float(v) if v else None
+        except (OSError, ValueError):
+            traffic = None
+    return {
+        "value": samples / elapsed, "ms_per_step": elapsed / steps * 1e3, "B": B, "batches": batches,
+        "active_fraction": a,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": dominant,
+                     "kernel_avg_us": avg_ms * 1e3, "algorithmic_bytes_per_launch": bytes_per_launch,
+                     "kernels_avg_us": kernels_us, "step_achieved_GBs": per_sample * samples / elapsed / 1e9},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -128,7 +242,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", default="transe_fb15k", choices=sorted(CONFIGS))
     ap.add_argument("--precision", type=int, default=64, choices=[32, 64])
-    ap.add_argument("--schedule", default="ordered", choices=["ordered", "parallel"])
+    ap.add_argument("--schedule", default="parallel", choices=["ordered", "parallel"],
+                    help="schedule of the headline value; the other one is reported beside it")
+    ap.add_argument("--only", action="store_true", help="measure the --schedule only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -143,121 +259,45 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
 
-    from kb2e_amd.engine import Engine
-
     model, shape, dim, method, distance, rate = CONFIGS[args.config]
     ds = data.synthetic(shape, seed=0)
     train = shard_heads(ds.train, rank, world) if world > 1 else ds.train
-    batches = 100
-    eng = Engine(model, dim, ds.num_entities, ds.num_relations, rate=rate, method=method, distance=distance,
-                 batches=batches, seed=7 + rank, precision=args.precision, device=local if world > 1 else 0,
-                 schedule=args.schedule)
-    eng.upload_triples(train)
-    ent, rel, w = eng.init_params()
-    if model == "R":
-        eng.transr_seed(ent, rel)  # seed = the init draws (no TransE run in the bench)
-    B = len(train) // batches
-    merger = None
-    if world > 1:
-        from kb2e_amd.distributed import EpochMerger
-        merger = EpochMerger(eng, dist)
-
-    def run(steps):
-        done = 0
-        while done < steps:
-            k = min(steps - done, batches - (run.pos % batches))
-            eng.train_batches(k)
-            done += k
-            run.pos += k
-            if merger is not None and run.pos % batches == 0:
-                merger.merge()
-    run.pos = 0
-
-    run(args.warmup)
-    eng.synchronize()
-    eng.take_stats()
-    # HIP-event timing of the batch kernels on every 10th batch (events cost
-    # device time; sampling keeps the timed run unperturbed)
-    eng.profile(10)
-    if dist is not None:
-        dist.barrier()
-    t0 = time.perf_counter()
-    run(args.steps)
-    eng.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    loss, active = eng.take_stats()
-    # phase B: TransE runs the per-row fold and the long-row fold concurrently
-    # (timed together as "fold_phase"); TransH/TransR run the relation owners.
-    fold_ms, fold_n = eng.profile_query("fold_phase" if model == "E" else "relowner")
-    kernels_us = {}
-    for k in (("score", "fold", "fold_long", "apply", "apply_long") if model == "E" else ("score", "tickets", "desc", "relowner")):
-        ms, n = eng.profile_query(k)
-        if n:
-            kernels_us[k] = ms / n * 1e3
-    score_ms, score_n = eng.profile_query("score")
-    samples = args.steps * B
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([elapsed, float(samples), float(active)], dtype=torch.float64, device="cuda")
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        elapsed = float(mx[0])
-        samples = float(t[1])
-        active = float(t[2])
+    main_run = measure(args, args.schedule, ds, train, rank, world, local, dist, args.steps, args.warmup)
+    other = "ordered" if args.schedule == "parallel" else "parallel"
+    other_run = None
+    if not args.only:
+        other_run = measure(args, other, ds, train, rank, world, local, dist, args.steps, args.warmup)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
-
-    a = active / max(1.0, samples)
-    s = 8 if args.precision == 64 else 4
-    per_sample, score_bytes, fold_bytes = algorithmic_bytes_per_sample(model, dim, s, a)
-    dominant = ("fold_phase" if model == "E" else "relowner") if fold_ms >= score_ms else "score"
-    if dominant == "score":
-        avg_ms, bytes_per_launch = score_ms / max(1, score_n), score_bytes * B
-    else:
-        avg_ms, bytes_per_launch = fold_ms / max(1, fold_n), fold_bytes * B
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}_f{args.precision}.json")
-    if os.path.exists(pmc):
-        try:
-            fams = json.load(open(pmc))
-            parts = ("fold", "fold_long") if dominant == "fold_phase" else (dominant,)
-            vals = [fams.get(p, {}).get("hbm_bytes_per_launch") for p in parts]
-            traffic = sum(v for v in vals if v) if any(vals) else None
-        except (OSError, ValueError):
-            traffic = None
+    B, batches = main_run["B"], main_run["batches"]
     out = {
         "metric": "training triples/sec (1/2/4/8 MI355X) + FB15k Hits@10(Filter)",
-        "value": samples / elapsed,
+        "value": main_run["value"],
         "unit": "triples/s (1 triple = 1 positive + 1 corrupted)",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": main_run["ms_per_step"],
         "higher_is_better": True,
-        # the FB15k-shaped triple set is fixed and sharded by head-entity hash over
-        # the ranks (each rank: 1/N of the triples, batches of 1/N the size), so
-        # total work per step is fixed as N grows
-        "scaling": "strong",
+        # every rank runs batches of the single-GPU size over its head-hash shard
+        "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64" if args.precision == 64 else "f32",
         "data": f"synthetic {shape}-shaped (kb2e_amd.data.synthetic, seed 0), reference glibc sample stream seed 7",
         "config": {"workload": f"{args.config}: {'TransE' if model == 'E' else 'TransH' if model == 'H' else 'TransR'} "
-                               f"n={dim} {'bern' if method else 'unif'} L{distance + 1}, {batches} batches of {B}",
-                   "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "single"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": dominant,
-                     "kernel_avg_us": avg_ms * 1e3, "algorithmic_bytes_per_launch": bytes_per_launch,
-                     "kernels_avg_us": kernels_us,
-                     "step_achieved_GBs": per_sample * samples / elapsed / 1e9},
-        "active_fraction": a,
+                               f"n={dim} {'bern' if method else 'unif'} L{distance + 1}, {batches} batches of {B} "
+                               f"per GPU, {args.schedule} schedule",
+                   "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "single",
+                   "schedule": args.schedule},
+        "roofline": main_run["roofline"],
+        "active_fraction": main_run["active_fraction"],
     }
+    if other_run is not None:
+        out["schedules"] = {args.schedule: {"value": main_run["value"], "ms_per_step": main_run["ms_per_step"]},
+                            other: {"value": other_run["value"], "ms_per_step": other_run["ms_per_step"],
+                                    "roofline": other_run["roofline"]}}
     if not args.no_cpu_baseline and world == 1:
         try:
             out["cpu_baseline"] = cpu_baseline(args.config, ds)

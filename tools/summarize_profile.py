@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """Summarise a tools/gpu_profile.sh run into profiles/ (committed evidence).
 
-Writes profiles/<tag>_<config>.md (kernel stats table + PMC traffic) and
-profiles/pmc_<config>_f<prec>.json (per-launch HBM bytes per kernel family,
-read by bench.py for roofline.traffic).
+Writes profiles/<tag>_<config>_<schedule>_f<prec>.md (kernel stats table + PMC
+traffic) and profiles/pmc_<config>_<schedule>_f<prec>.json (HBM bytes per batch
+of each phase bench.py times -- "score", "fold_phase", "apply", "relowner" --
+and per launch of each kernel family; read by bench.py for roofline.traffic).
+The PMC passes run `batches` batches (warmup + steps of the pass).
 
 HBM bytes per MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE are in KiB;
 on gfx950 FETCH_SIZE counts exactly half of a wide coalesced read, so the
@@ -22,6 +24,14 @@ FAMILY = {"transe_fold_long_kernel": "fold_long", "transe_fold_kernel": "fold", 
           "relowner_desc": "desc", "relowner_compact": "desc", "transr_commit": "commit"}
 
 
+# kernel -> the bench.py phase it belongs to (the HIP-event spans of the engine)
+PHASE = [("transe_score", "score"), ("transh_score", "score"), ("transr_project", "score"),
+         ("transr_compat", "score"), ("transr_tile", "score"), ("rpar_scan", "score"),
+         ("transe_fold", "fold_phase"), ("transe_apply", "fold_phase|apply"), ("transh_w_apply", "fold_phase"),
+         ("transh_orth", "fold_phase"), ("transr_rel_rows", "apply"), ("transr_entity", "apply"),
+         ("transr_constraint", "apply"), ("owner_kernel", "relowner"), ("owner_reg_kernel", "relowner")]
+
+
 def family(name):
     for k, v in FAMILY.items():
         if k in name:
@@ -29,7 +39,15 @@ def family(name):
     return name
 
 
-def main(src, tag, config, prec):
+def phase(name):
+    for k, v in PHASE:
+        if k in name:
+            return v
+    return None
+
+
+def main(src, tag, config, prec, schedule="parallel", batches="120"):
+    nbatch = float(batches)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
     bench = open(os.path.join(src, "bench.json")).read().strip()
@@ -39,19 +57,29 @@ def main(src, tag, config, prec):
         if not os.path.exists(path):
             continue
         agg = defaultdict(lambda: [0.0, 0])
+        ph = defaultdict(float)
         for r in csv.DictReader(open(path)):
             a = agg[family(r["Kernel_Name"])]
             a[0] += float(r["Counter_Value"])
             a[1] += 1
+            p = phase(r["Kernel_Name"])
+            for q in (p.split("|") if p else []):
+                ph[q] += float(r["Counter_Value"])
         pmc[c] = {k: v[0] / max(1, v[1]) for k, v in agg.items()}  # KiB per launch
+        pmc[c + "_phase"] = {k: v / nbatch for k, v in ph.items()}  # KiB per batch
     per_kernel = {}
     for fam in set(pmc.get("FETCH_SIZE", {})) | set(pmc.get("WRITE_SIZE", {})):
         f = pmc.get("FETCH_SIZE", {}).get(fam, 0.0) * 1024
         w = pmc.get("WRITE_SIZE", {}).get(fam, 0.0) * 1024
         per_kernel[fam] = {"fetch_bytes_raw": f, "write_bytes": w, "hbm_bytes_per_launch": 2 * f + w}
-    out_json = os.path.join(root, "profiles", f"pmc_{config}_f{prec}.json")
+    for p in set(pmc.get("FETCH_SIZE_phase", {})) | set(pmc.get("WRITE_SIZE_phase", {})):
+        f = pmc.get("FETCH_SIZE_phase", {}).get(p, 0.0) * 1024
+        w = pmc.get("WRITE_SIZE_phase", {}).get(p, 0.0) * 1024
+        per_kernel[p] = {"fetch_bytes_raw": f, "write_bytes": w, "hbm_bytes_per_launch": 2 * f + w,
+                         "note": "phase total per batch"}
+    out_json = os.path.join(root, "profiles", f"pmc_{config}_{schedule}_f{prec}.json")
     json.dump(per_kernel, open(out_json, "w"), indent=1, sort_keys=True)
-    lines = [f"# Profile {tag}: {config} (f{prec})", "", "Command: `tools/gpu_profile.sh` on one MI355X "
+    lines = [f"# Profile {tag}: {config}, {schedule} schedule (f{prec})", "", "Command: `tools/gpu_profile.sh` on one MI355X "
              "(rocprofv3 --kernel-trace --stats; separate --pmc FETCH_SIZE / WRITE_SIZE passes).", "",
              "## bench.py line", "", "```", bench, "```", "", "## Kernel stats (rocprofv3 --stats)", "",
              "| kernel | calls | total ms | avg us | % |", "|---|---|---|---|---|"]
@@ -62,10 +90,10 @@ def main(src, tag, config, prec):
               "| kernel family | FETCH_SIZE raw (bytes) | WRITE_SIZE (bytes) | corrected HBM bytes |", "|---|---|---|---|"]
     for fam, v in sorted(per_kernel.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"])[:12]:
         lines.append(f"| {fam} | {v['fetch_bytes_raw']:.0f} | {v['write_bytes']:.0f} | {v['hbm_bytes_per_launch']:.0f} |")
-    md = os.path.join(root, "profiles", f"{tag}_{config}_f{prec}.md")
+    md = os.path.join(root, "profiles", f"{tag}_{config}_{schedule}_f{prec}.md")
     open(md, "w").write("\n".join(lines) + "\n")
     print(md, out_json)
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:7])
