@@ -155,7 +155,7 @@ struct kb2e_ctx {
     DevBuf aux, aux2;      // model-specific per-update exports
     // relation-owner schedule (TransH / TransR)
     RelOwnerPlan plan;
-    DevBuf owner, tickets, ent_done, wsnap, transr_work, owner_seg, dataflow_err, wtouched, desc, cdesc, ocount;
+    DevBuf owner, tickets, ent_done, wsnap, transr_work, transr_work_alt, owner_seg, dataflow_err, wtouched, desc, cdesc, ocount;
     int num_cus = 256;
     uint32_t batch_stamp = 0;
     int32_t gram_min = 48;  // KB2E_GRAM_MIN: fold segments this long use the scalar recurrence (0 = off)
@@ -170,6 +170,7 @@ struct kb2e_ctx {
     int32_t rpar_St = 8, rpar_max_tiles = 1;
     bool rpar_no_constraint = false;
     bool rpar_mfma = false;  // matrix-core tile kernels (kernels_transr_mfma.hpp)
+    DevBuf rpar_pflag, rpar_cons_tile;
     DevBuf rpar_y, rpar_wpart, rpar_rpart, rpar_tile_act, rpar_pair, rpar_relpair, rpar_relpair_stamp, rpar_tiles,
         rpar_ntiles, rpar_tile_first, rpar_rel_begin, rpar_scan;
     hipStream_t fold_stream = nullptr;  // the long-segment fold runs beside the per-row fold
@@ -1310,12 +1311,8 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
         if (getenv("KB2E_RPAR_STATS")) {  // transRNorm rounds of the PARALLEL TransR schedule
             unsigned long long st[8];
             HIPCHK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_rpar_rounds), sizeof(st)));
-            fprintf(stderr,
-                    "rpar_rounds max-per-tile sum %llu tiles %llu max %llu cycles/tile setup %.0f rounds %.0f (gemm1 %.0f "
-                    "-- %.0f) final %.0f\n",
-                    st[0], st[1], st[2], (double)st[3] / std::max(1ull, st[1]), (double)st[4] / std::max(1ull, st[1]),
-                    (double)st[6] / std::max(1ull, st[1]), (double)st[7] / std::max(1ull, st[1]),
-                    (double)st[5] / std::max(1ull, st[1]));
+            fprintf(stderr, "rpar_rounds rounds of row blocks %llu, tiles with violators %llu, most rounds of a block %llu\n",
+                    st[0], st[1], st[2]);
             std::memset(st, 0, sizeof(st));
             HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_rpar_rounds), st, sizeof(st)));
         }

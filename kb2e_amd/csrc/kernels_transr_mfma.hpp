@@ -81,13 +81,13 @@ __host__ __device__ constexpr size_t rmfma_tile_lds(int n, int St) {
            sizeof(int) * ((size_t)rm_up16(4 * St) + St);
 }
 
-// transRNorm kernel LDS: W [NP][L] | WT [NP][L] | A [PP][L] | G [PP][L] | Pm [PP][L] | s0 [PP] |
-// int ent_of [PP], live [PP] | counter | kk [St], act [St]
+// transRNorm kernel LDS: W [NP][L] | K [NP][L] | A0 [PP][L] | PG [PP][L] | s0 [PP] |
+// int ent_of, slot_of, rowmap, posmap, vio [PP] | 4
 template <typename T>
 __host__ __device__ constexpr size_t rmfma_cons_lds(int n, int St) {
-    return sizeof(T) * (2 * (size_t)rm_np(n) * rm_ld(n) + 3 * (size_t)rm_up16(4 * St + 1) * rm_ld(n) +
+    return sizeof(T) * (2 * (size_t)rm_np(n) * rm_ld(n) + 2 * (size_t)rm_up16(4 * St + 1) * rm_ld(n) +
                         rm_up16(4 * St + 1)) +
-           sizeof(int) * (2 * (size_t)rm_up16(4 * St + 1) + 4 + 2 * (size_t)St);
+           sizeof(int) * (5 * (size_t)rm_up16(4 * St + 1) + 4);
 }
 
 template <typename T>
@@ -301,34 +301,44 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
     }
 }
 
-// transRNorm per tile on the matrix cores, pairs and rules of
-// transr_constraint_kernel; all pairs of the tile advance together, a Jacobi
-// round per loop trip, until none violates.
-// transRNorm statistics (tools): rounds summed over tiles, tiles, most rounds in a tile
-__device__ unsigned long long g_rpar_rounds[8];  // + [3..6]: cycles per phase summed over tiles
+// transRNorm (transr/trainer.cpp:35-64) per tile on the matrix cores, pairs and
+// rules of transr_constraint_kernel: the pairs (h', r), (t', r) of the tile's
+// active updates and (entity'[r], r) on the relation's first tile, first
+// occurrences only, compacted.  With W0 = W'_r and K = W0^T W0 (MFMA, once):
+//   P = A0 W0 for all pairs (MFMA), |p|^2 reduced from the accumulators;
+//   Jacobi rounds on the violators, one wave per 16-row block with its P and
+//   G fragments in registers:  G += 2 p,  p <- p - 2 lr K p - 2 lr (a0.a0) p
+//   while |p|^2 > 1 (a row stops at its own first non-violation);
+//   pair records da = -lr W0 G (MFMA), the tile's matrix partial -lr A0^T G
+//   (MFMA), a flag per update slot (bf.pflag: the record is valid) and the
+//   tile's violator count (bf.cons_tile: 0 = no partial).
+// transRNorm statistics (tools): rounds summed over row blocks, tiles with violators, most rounds of a block
+__device__ unsigned long long g_rpar_rounds[8];
 
-template <typename T>
-__global__ __launch_bounds__(512) void transr_constraint_mfma_kernel(RParArgs a, RParBufs<T> bf) {
+// kConsNB: column blocks of 16 held in registers (NP / 16 <= kConsNB)
+template <typename T, int kConsNB>
+__global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParBufs<T> bf) {
+    using M = Mfma16<T>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int t = a.tile_first[a.batch_seg[a.batch]] + blockIdx.x;
+    const int tb = a.tile_first[a.batch_seg[a.batch]];
+    const int t = tb + blockIdx.x;
     if (t >= a.tile_first[a.batch_seg[a.batch + 1]]) return;
     int r, e0, cnt;
     tile_range(a, t, r, e0, cnt);
-    const int n = a.n, ld = a.ld, NP = rm_np(n), L = rm_ld(n);
+    const int n = a.n, ld = a.ld, NP = rm_np(n), L = rm_ld(n), NB = NP / 16;
     const int PP = rm_up16(4 * a.St + 1);
     T* Wl = (T*)smem;
-    T* WT = Wl + NP * L;  // W transposed: lane-contiguous rows for W x
-    T* A = WT + NP * L;
-    T* G = A + PP * L;
-    T* Pm = G + PP * L;
-    T* s0 = Pm + PP * L;
+    T* K = Wl + NP * L;
+    T* A0 = K + NP * L;
+    T* PG = A0 + PP * L;  // P during the rounds, then G
+    T* s0 = PG + PP * L;
     int* ent_of = (int*)(s0 + PP);
-    int* live = ent_of + PP;
-    int* nactive = live + PP;
-    int* kks = nactive + 4;  // sample index of every tile sample
-    int* acts = kks + a.St;  // its hinge flag
+    int* slot_of = ent_of + PP;  // pair slot (kk * 2 + u) * 2 + role, -2 for (entity[r], r), -1 none
+    int* rowmap = slot_of + PP;  // compacted row -> pq
+    int* posmap = rowmap + PP;   // pq -> compacted row or -1
+    int* vio = posmap + PP;      // compacted row violates (its pair moves)
+    int* misc = vio + PP;        // [0] live rows, [1] violators
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = lane_id();
-    const unsigned long long t_start = clock64();
     const RTile tl = a.tiles[t];
     bool relpair = false;
     if (tl.q == 0) {
@@ -338,130 +348,202 @@ __global__ __launch_bounds__(512) void transr_constraint_mfma_kernel(RParArgs a,
     }
     const int npairs = 4 * cnt + (relpair ? 1 : 0);
     for (int pq = threadIdx.x; pq < PP; pq += blockDim.x) {
-        int ent = -1;
+        int ent = -1, slot = -1;
         if (pq < 4 * cnt) {
             const int q = pq >> 2, u = (pq >> 1) & 1, role = pq & 1;
             const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
-            const int ac = a.act[kk];
-            if ((pq & 3) == 0) {
-                kks[q] = kk;
-                acts[q] = ac;
-            }
-            if (ac) {
+            if (a.act[kk]) {
                 const int i0 = a.si[kk], jj = a.sj[kk];
                 const int h = a.heads[i0], tt = a.tails[i0];
                 const int hh = u ? (a.side[kk] ? h : jj) : h;
                 const int th = u ? (a.side[kk] ? jj : tt) : tt;
                 ent = role ? th : hh;
+                slot = (kk * 2 + u) * 2 + role;
             }
         } else if (pq < npairs) {
             ent = r;  // entityVec_next_[relation] (transr/trainer.cpp:187)
+            slot = -2;
         }
         ent_of[pq] = ent;
+        slot_of[pq] = slot;
+        vio[pq] = 0;
     }
     stage_matrix_padded(Wl, bf.W + (int64_t)r * n * ld, n, ld);
+    if (threadIdx.x == 0) misc[1] = 0;
     __syncthreads();
-    for (int idx = threadIdx.x; idx < NP * L; idx += blockDim.x) {
-        const int j = idx / L, i = idx % L;
-        WT[idx] = (j < NP && i < NP) ? Wl[i * L + j] : T(0);
+    if (w == 0) {  // first occurrence of each entity, compacted in pair order
+        int base = 0;
+        for (int p0 = 0; p0 < PP; p0 += kWave) {
+            const int pq = p0 + l;
+            const int ent = pq < PP ? ent_of[pq] : -1;
+            bool dup = false;
+            const int kmax = min(PP, p0 + kWave);  // PP is a multiple of 16
+            for (int k = 0; k < kmax; k += 4) {
+                const int4 e4 = *(const int4*)(ent_of + k);
+                dup |= (k < pq && e4.x == ent) | (k + 1 < pq && e4.y == ent) | (k + 2 < pq && e4.z == ent) |
+                       (k + 3 < pq && e4.w == ent);
+            }
+            const bool live = ent >= 0 && !dup;
+            const uint64_t m = __ballot(live);
+            const int pos = base + __builtin_popcountll(m & ((1ull << l) - 1));
+            if (live) rowmap[pos] = pq;
+            if (pq < PP) posmap[pq] = live ? pos : -1;
+            base += __builtin_popcountll(m);
+        }
+        if (l == 0) misc[0] = base;
     }
-    for (int pq = threadIdx.x; pq < PP; pq += blockDim.x) {  // first occurrence of each entity in the tile
-        const int ent = ent_of[pq];
-        bool lv = ent >= 0;
-        for (int k = 0; lv && k < pq; ++k) lv = ent_of[k] != ent;
-        live[pq] = lv ? ent : -1;  // the row's entity, or -1
+    __syncthreads();
+    const int nrows = misc[0];
+    const int MR = rm_up16(nrows);
+    for (int idx = threadIdx.x; idx < MR * L; idx += blockDim.x) {
+        const int row = idx / L, i = idx % L;
+        const int e = row < nrows ? ent_of[rowmap[row]] : -1;
+        A0[idx] = (e >= 0 && i < n) ? bf.ent[(int64_t)e * ld + i] : T(0);
     }
     __syncthreads();
-    for (int idx = threadIdx.x; idx < PP * L; idx += blockDim.x) G[idx] = T(0);
-    gather_rows(A, live, PP, bf.ent, n, ld);
-    __syncthreads();
-    for (int row = w; row < PP; row += nw) {
-        T ss = T(0);
-        for (int i = l; i < L; i += kWave) ss += A[row * L + i] * A[row * L + i];
-        ss = wave_sum(ss);
-        if (l == 0) s0[row] = ss;
+    if (nrows > 0) {
+        // K = W0^T W0 (symmetric, zero past n) and s0 = a0.a0
+        block_gemm<T>(NB, NB, NP, [&](int m, int k) { return Wl[k * L + m]; },
+                      [&](int k, int c) { return Wl[k * L + c]; }, [&](int m, int c, T v) { K[m * L + c] = v; });
+        for (int row = w; row < nrows; row += nw) {
+            T ss = T(0);
+            for (int i = l; i < L; i += kWave) ss += A0[row * L + i] * A0[row * L + i];
+            ss = wave_sum(ss);
+            if (l == 0) s0[row] = ss;
+        }
     }
     __syncthreads();
-    const unsigned long long t_setup = clock64();
     const T lr = (T)a.lr;
-    // p0 = W^T a0 for every pair at once (matrix cores)
-    block_gemm<T>(PP / 16, NP / 16, NP, [&](int m, int k) { return A[m * L + k]; },
-                  [&](int k, int c) { return Wl[k * L + c]; }, [&](int m, int c, T v) { Pm[m * L + c] = v; });
-    __syncthreads();
-    const unsigned long long t_g1 = clock64();
-    // Per violating pair, one wave runs the Jacobi rounds on the projection:
-    //   p_{m+1} = p_m - 2 lr W^T (W p_m) - 2 lr (a0.a0) p_m,   G += 2 p_m,
-    // equal to re-projecting a_{m+1} = a_m - lr W g_m under the shrunk W (first
-    // order in lr); then da = -lr W G.  No block barrier inside the rounds.
-    int rounds = 0;
-    for (int row = w; row < PP; row += nw) {
-        const bool lv = live[row] >= 0;
-        T p[2], g2[2] = {T(0), T(0)};
+    // one wave per 16-row block: P0 = A0 W0, then the rounds on its violators
+    for (int mb = w; mb < MR / 16; mb += nw) {
+        typename M::acc_t pf[kConsNB], gf[kConsNB];
+        const int ar = mb * 16 + (l & 15), kq = l >> 4;
+        auto rowsq = [&](T (&nrm)[4]) {  // |p|^2 of the lane's four rows
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int i = 2 * l + k;
-            p[k] = (lv && i < n) ? Pm[row * L + i] : T(0);
+            for (int q = 0; q < 4; ++q) nrm[q] = T(0);
+#pragma unroll
+            for (int nb = 0; nb < kConsNB; ++nb) {
+                if (nb >= NB) break;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    T v = pf[nb][q] * pf[nb][q];
+                    v += dpp_ror<8>(v);
+                    v += dpp_ror<4>(v);
+                    v += dpp_ror<2>(v);
+                    v += dpp_ror<1>(v);
+                    nrm[q] += v;
+                }
+            }
+        };
+        auto mul = [&](const T* Aop, const T* Bop, typename M::acc_t (&out)[kConsNB]) {  // rows of Aop (this block) x Bop
+#pragma unroll
+            for (int nb = 0; nb < kConsNB; ++nb) {
+                if (nb >= NB) break;
+                typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
+                const int bc = nb * 16 + (l & 15);
+                for (int kb = 0; kb < NP; kb += 32) {
+                    T av[8], bv[8];
+#pragma unroll
+                    for (int s8 = 0; s8 < 8; ++s8) {
+                        const int k = kb + 4 * s8 + kq;
+                        const bool ok = kb + 4 * s8 < NP;
+                        av[s8] = ok ? Aop[ar * L + k] : T(0);
+                        bv[s8] = ok ? Bop[k * L + bc] : T(0);
+                    }
+#pragma unroll
+                    for (int s8 = 0; s8 < 8; ++s8) acc = M::mma(av[s8], bv[s8], acc);
+                }
+                out[nb] = acc;
+            }
+        };
+        mul(A0, Wl, pf);
+        T nrm[4], cc[4];
+        bool live[4];
+        rowsq(nrm);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = mb * 16 + M::row(l, q);
+            live[q] = row < nrows && nrm[q] > T(1);
+            cc[q] = row < nrows ? T(2) * lr * s0[row] : T(0);
         }
-        T* vrow = Pm + row * L;  // this row's scratch: p broadcast, then W p
+#pragma unroll
+        for (int nb = 0; nb < kConsNB; ++nb) gf[nb] = {T(0), T(0), T(0), T(0)};
+        if ((l & 15) == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (live[q]) vio[mb * 16 + M::row(l, q)] = 1;
+        }
         int m = 0;
-        for (; lv && m < kRParMaxIter; ++m) {
-            const T xx = wave_sum(p[0] * p[0] + p[1] * p[1]);
-            if (!(xx > T(1))) break;
-            g2[0] += T(2) * p[0];
-            g2[1] += T(2) * p[1];
-            lane_pair_store(vrow, n, p);
-            wave_lds_sync();
-            T v[2];
-            matvec_t(WT, L, n, vrow, v);  // v = W p
-            wave_lds_sync();
-            lane_pair_store(vrow, n, v);
-            wave_lds_sync();
-            T q[2];  // q = W^T v: the same product on the untransposed image
-            matvec_t(Wl, L, n, vrow, q);
-            wave_lds_sync();
-            const T c = T(2) * lr * s0[row];
+        for (; m < kRParMaxIter; ++m) {
+            if (!__ballot(live[0] || live[1] || live[2] || live[3])) break;
 #pragma unroll
-            for (int k = 0; k < 2; ++k) p[k] = 2 * l + k < n ? p[k] - T(2) * lr * q[k] - c * p[k] : T(0);
+            for (int nb = 0; nb < kConsNB; ++nb) {
+                if (nb >= NB) break;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (live[q]) gf[nb][q] += T(2) * pf[nb][q];
+                    PG[(mb * 16 + M::row(l, q)) * L + nb * 16 + (l & 15)] = pf[nb][q];
+                }
+            }
+            typename M::acc_t qf[kConsNB];
+            wave_lds_sync();
+            mul(PG, K, qf);  // K p
+            wave_lds_sync();
+#pragma unroll
+            for (int nb = 0; nb < kConsNB; ++nb) {
+                if (nb >= NB) break;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    pf[nb][q] = live[q] ? pf[nb][q] - T(2) * lr * qf[nb][q] - cc[q] * pf[nb][q] : pf[nb][q];
+            }
+            rowsq(nrm);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) live[q] = live[q] && nrm[q] > T(1);
         }
-        rounds = max(rounds, m);
-        lane_pair_store(G + row * L, n, g2);  // G = sum of g_m (zero if the pair never violated)
-        if (l == 0) live[row] = m > 0 ? 1 : 0;  // from here on: the pair moved
+#pragma unroll
+        for (int nb = 0; nb < kConsNB; ++nb) {
+            if (nb >= NB) break;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) PG[(mb * 16 + M::row(l, q)) * L + nb * 16 + (l & 15)] = gf[nb][q];
+        }
+        if (l == 0 && m > 0) {
+            atomicAdd(&misc[1], 1);
+            if (bf.stats) {
+                atomicAdd(&g_rpar_rounds[0], (unsigned long long)m);
+                atomicMax(&g_rpar_rounds[2], (unsigned long long)m);
+            }
+        }
     }
     __syncthreads();
-    const unsigned long long t_rounds = clock64();
-    if (threadIdx.x == 0) {
-        atomicAdd(&g_rpar_rounds[3], t_setup - t_start);
-        atomicAdd(&g_rpar_rounds[4], t_rounds - t_setup);
-        atomicAdd(&g_rpar_rounds[6], t_g1 - t_setup);
-        atomicAdd(&g_rpar_rounds[0], (unsigned long long)rounds);
-        atomicAdd(&g_rpar_rounds[1], 1ull);
-        atomicMax(&g_rpar_rounds[2], (unsigned long long)rounds);
-    }
-    // pair records: da = -lr W G; the matrix step uses -lr a0 (A still holds a0)
-    for (int row = w; row < PP; row += nw) {
-        T da[2] = {T(0), T(0)};
-        if (live[row]) {
-            matvec_t(WT, L, n, G + row * L, da);
-            da[0] *= -lr;
-            da[1] *= -lr;
+    if (w == 0) {  // pair flags and the tile's entry
+        for (int pq = l; pq < 4 * cnt; pq += kWave) {
+            const int slot = slot_of[pq];
+            if (slot < 0) continue;
+            const int pos = posmap[pq];
+            bf.pflag[slot] = pos >= 0 && vio[pos] ? 1 : 0;
         }
-        if (row < 4 * cnt) {
-            const int q = row >> 2, u = (row >> 1) & 1, role = row & 1;
-            if (acts[q]) lane_pair_store(bf.pair + (((int64_t)kks[q] * 2 + u) * 2 + role) * ld, n, da);
-        } else if (row < npairs) {
-            lane_pair_store(bf.relpair + (int64_t)r * ld, n, da);
-            if (l == 0) bf.relpair_stamp[r] = bf.stamp;
+        if (l == 0) {
+            bf.cons_tile[blockIdx.x] = misc[1];
+            if (misc[1] && bf.stats) atomicAdd(&g_rpar_rounds[1], 1ull);
         }
     }
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < PP * L; idx += blockDim.x) A[idx] *= -lr;
-    __syncthreads();
-    T* wp = bf.wpart + (int64_t)blockIdx.x * n * ld;
-    block_gemm<T>(NP / 16, NP / 16, PP, [&](int j, int p) { return A[p * L + j]; },
-                  [&](int p, int i) { return G[p * L + i]; }, [&](int j, int i, T v) {
-                      if (j < n && i < n) wp[(int64_t)j * ld + i] = v;
+    if (misc[1] == 0) return;
+    // pair records da = -lr W0 G (B(k, c) = W0[c][k])
+    block_gemm<T>(MR / 16, NB, NP, [&](int m, int k) { return PG[m * L + k]; },
+                  [&](int k, int c) { return Wl[c * L + k]; }, [&](int m, int c, T v) {
+                      if (m >= nrows || c >= n || !vio[m]) return;
+                      const int sl = slot_of[rowmap[m]];
+                      if (sl >= 0) bf.pair[(int64_t)sl * ld + c] = -lr * v;
+                      else bf.relpair[(int64_t)r * ld + c] = -lr * v;
                   });
-    if (threadIdx.x == 0) atomicAdd(&g_rpar_rounds[5], clock64() - t_rounds);
+    for (int row = threadIdx.x; row < nrows; row += blockDim.x)
+        if (vio[row] && slot_of[rowmap[row]] == -2) bf.relpair_stamp[r] = bf.stamp;
+    // the tile's matrix partial  dW[j][i] = sum_p (-lr a0[p][j]) G[p][i]
+    T* wp = bf.wpart + (int64_t)blockIdx.x * n * ld;
+    block_gemm<T>(NB, NB, MR, [&](int j, int p) { return A0[p * L + j]; }, [&](int p, int i) { return PG[p * L + i]; },
+                  [&](int j, int i, T v) {
+                      if (j < n && i < n) wp[(int64_t)j * ld + i] = -lr * v;
+                  });
 }
 
 }  // namespace kb2e

@@ -77,7 +77,13 @@ struct RParBufs {
     T* relpair;  // [R][ld] transRNorm delta of (entity[r], r)
     uint32_t* relpair_stamp;  // [R] batch stamp when relpair[r] is valid this batch
     uint32_t stamp;
+    // matrix-core transRNorm (kernels_transr_mfma.hpp); null on the VALU path
+    uint8_t* pflag;      // [B][2][2] the pair record of the slot is valid this batch
+    int32_t* cons_tile;  // [tiles] row blocks with violators per tile (0: no matrix partial)
+    int32_t stats;       // count transRNorm rounds (tools)
 };
+
+__host__ __device__ constexpr int rm_up16_host_dev(int v) { return (v + 15) & ~15; }
 
 template <typename T>
 __host__ __device__ constexpr int rpar_lds_w(int n, int ld) {
@@ -332,23 +338,29 @@ __global__ __launch_bounds__(256) void transr_rel_rows_kernel(RParArgs a, RParBu
     const int r = a.seg_row[s] - a.ne;
     const int t0 = a.tile_first[s], t1 = a.tile_first[s + 1];
     const int n = a.n, ld = a.ld;
-    int any = 0;  // the reference touches (and normalises) a relation only through an active update
-    for (int t = t0; t < t1; ++t) any |= a.tile_act[t];
+    const int tb = a.tile_first[a.batch_seg[a.batch]];  // partials are indexed by tile within the batch
+    // GRAD step: the reference touches (and normalises) a relation only through
+    // an active update; matrix-core transRNorm step: only tiles whose pairs moved
+    // have a partial
+    const bool sel = !NORM && bf.cons_tile;
+    int any = 0;
+    for (int t = t0; t < t1; ++t) any |= sel ? bf.cons_tile[t - tb] : a.tile_act[t];
     if (!any) return;
     T* row = j < n ? bf.W + ((int64_t)r * n + j) * ld : bf.rel + (int64_t)r * ld;
     T v[2];
     lane_pair_load(row, n, v);
-    const int tb = a.tile_first[a.batch_seg[a.batch]];  // partials are indexed by tile within the batch
     for (int t = t0; t < t1; t += 4) {  // four partial rows in flight, summed in tile order
         T p[4][2];
+        bool use[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int64_t lt = t + q - tb;
-            if (t + q < t1) lane_pair_load(j < n ? bf.wpart + (lt * n + j) * ld : bf.rpart + lt * ld, n, p[q]);
+            use[q] = t + q < t1 && (!sel || bf.cons_tile[lt] != 0);
+            if (use[q]) lane_pair_load(j < n ? bf.wpart + (lt * n + j) * ld : bf.rpart + lt * ld, n, p[q]);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            if (t + q < t1) {
+            if (use[q]) {
                 v[0] += p[q][0];
                 v[1] += p[q][1];
             }
@@ -523,12 +535,15 @@ __device__ __forceinline__ void rpar_entity_events(const RParArgs& a, const RPar
                         src = kk * 2 + u;
                         c = (T)((hd ? -1.0 : 1.0) * (u ? 1.0 : -1.0) * a.lr);
                     }
-                } else {
-                    nrm = hd || tl;
-                    if (hd) src = (kk * 2 + u) * 2 + 0;
-                    if (tl) {
-                        if (src < 0) src = (kk * 2 + u) * 2 + 1;
-                        else src2 = (kk * 2 + u) * 2 + 1;
+                } else {  // pair records; with flags only those whose pair moved
+                    const int s0 = (kk * 2 + u) * 2;
+                    const bool ph = hd && (!bf.pflag || bf.pflag[s0]);
+                    const bool pt = tl && (!bf.pflag || bf.pflag[s0 + 1]);
+                    nrm = ph || pt;
+                    if (ph) src = s0;
+                    if (pt) {
+                        if (src < 0) src = s0 + 1;
+                        else src2 = s0 + 1;
                     }
                 }
             }
@@ -636,9 +651,9 @@ __global__ __launch_bounds__(1024) void transr_entity_kernel(RParArgs a, RParBuf
 //
 // transr/transr.cpp:20-25 never zeroes the work vectors, so call c of the
 // batch (pos, neg of sample 0, then of sample 1, ...) sees work + the sum of
-// the projections of calls 0..c.  Three passes over chunks of kScanChunk calls
-// (chunk sums; prefix over chunks from the carried work vectors; inclusive scan
-// inside each chunk), one thread per (head/tail, element), coalesced rows.
+// the projections of calls 0..c.  Two passes over chunks of kScanChunk calls
+// (chunk sums; then per chunk its prefix, the inclusive scan inside it and the
+// energies), one thread per (head/tail, element), coalesced rows.
 constexpr int kScanChunk = 64;
 
 __global__ __launch_bounds__(256) void rpar_scan_sums_kernel(const double* proj, int64_t calls, int32_t ld,
@@ -647,36 +662,81 @@ __global__ __launch_bounds__(256) void rpar_scan_sums_kernel(const double* proj,
     const int64_t c0 = (int64_t)c * kScanChunk, c1 = min<int64_t>(calls, c0 + kScanChunk);
     for (int e = threadIdx.x; e < 2 * n; e += blockDim.x) {
         const int side = e / n, i = e % n;
-        double s = 0;
-        for (int64_t k = c0; k < c1; ++k) s += proj[(k * 2 + side) * ld + i];
-        sums[(int64_t)c * 2 * n + e] = s;
-    }
-}
-
-__global__ __launch_bounds__(256) void rpar_scan_prefix_kernel(double* sums, int32_t nchunks, int32_t n,
-                                                               double* work) {
-    for (int e = threadIdx.x; e < 2 * n; e += blockDim.x) {
-        double run = work[e];  // work = [head n][tail n]
-        for (int c = 0; c < nchunks; ++c) {
-            const double s = sums[(int64_t)c * 2 * n + e];
-            sums[(int64_t)c * 2 * n + e] = run;  // exclusive prefix
-            run += s;
+        // four interleaved partial sums: 16 independent loads in flight per step
+        double s[4] = {0, 0, 0, 0};
+        for (int64_t k = c0; k < c1; k += 16) {
+            double v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = k + q < c1 ? proj[((k + q) * 2 + side) * ld + i] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) s[q & 3] += v[q];
         }
-        work[e] = run;
+        sums[(int64_t)c * 2 * n + e] = (s[0] + s[1]) + (s[2] + s[3]);
     }
 }
 
-__global__ __launch_bounds__(256) void rpar_scan_apply_kernel(double* proj, int64_t calls, int32_t ld, int32_t n,
-                                                              const double* sums) {
-    const int c = blockIdx.x;
+// The chunk's exclusive prefix (work_in + the sums of all earlier chunks, each
+// block summing them itself: no serial pass over the chunks), the inclusive
+// scan inside the chunk (LDS), then the compat energies of the chunk's
+// kScanChunk / 2 samples (transr/transr.cpp:26-35 on the accumulated vectors)
+// and the hinge (common/trainer.cpp:138-141).  The last chunk leaves the work
+// vectors after the batch in work_out (ping-pong with work_in across batches).
+template <typename T>
+__global__ __launch_bounds__(256) void rpar_scan_energy_kernel(RParArgs a, RParBufs<T> bf, const double* sums,
+                                                               int32_t nchunks, const double* work_in,
+                                                               double* work_out) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double* run_l = (double*)smem;  // [kScanChunk][2 n]
+    const int c = blockIdx.x, n = a.n, ld = a.ld;
+    const int64_t calls = 2 * (int64_t)a.B;
     const int64_t c0 = (int64_t)c * kScanChunk, c1 = min<int64_t>(calls, c0 + kScanChunk);
     for (int e = threadIdx.x; e < 2 * n; e += blockDim.x) {
+        double s[4] = {0, 0, 0, 0};
+        for (int q0 = 0; q0 < c; q0 += 16) {
+            double v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = q0 + q < c ? sums[(int64_t)(q0 + q) * 2 * n + e] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) s[q & 3] += v[q];
+        }
+        double run = work_in[e] + ((s[0] + s[1]) + (s[2] + s[3]));
         const int side = e / n, i = e % n;
-        double run = sums[(int64_t)c * 2 * n + e];
-        for (int64_t k = c0; k < c1; ++k) {
-            double* p = proj + (k * 2 + side) * ld + i;
-            run += *p;
-            *p = run;
+        for (int64_t k = c0; k < c1; k += 16) {
+            double v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = k + q < c1 ? a.proj[((k + q) * 2 + side) * ld + i] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if (k + q < c1) {
+                    run += v[q];
+                    run_l[(k + q - c0) * 2 * n + e] = run;
+                }
+        }
+        if (c == nchunks - 1) work_out[e] = run;
+    }
+    __syncthreads();
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = lane_id();
+    for (int64_t kk = c0 / 2 + w; kk < c1 / 2; kk += nw) {
+        const int r = a.rels[a.si[kk]];
+        T vr[2];
+        lane_pair_load(bf.rel + (int64_t)r * ld, n, vr);
+        const double* pp = run_l + (kk * 2 - c0) * 2 * n;  // [pos: head n, tail n][neg: head n, tail n]
+        double ep = 0, en = 0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int i = 2 * l + k;
+            if (i >= n) continue;
+            const double dp = pp[n + i] - pp[i] - (double)vr[k];
+            const double dn = pp[3 * n + i] - pp[2 * n + i] - (double)vr[k];
+            ep += a.l1 ? fabs(dp) : dp * dp;
+            en += a.l1 ? fabs(dn) : dn * dn;
+        }
+        ep = wave_sum(ep);
+        en = wave_sum(en);
+        const bool active = ep + a.margin > en;
+        if (l == 0) {
+            a.act[kk] = active ? 1 : 0;
+            a.loss[kk] = active ? a.margin + ep - en : 0.0;
         }
     }
 }

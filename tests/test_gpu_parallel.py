@@ -113,7 +113,7 @@ def _transr_vs_model(ds, dim, epochs, monkeypatch, *, St=8, compat=False, distan
 
 
 @pytest.mark.parametrize("mfma", [True, False])
-@pytest.mark.parametrize("dim,distance,St", [(20, 0, 8), (20, 1, 4), (50, 0, 8), (33, 0, 2), (20, 0, 16), (64, 0, 1)])
+@pytest.mark.parametrize("dim,distance,St", [(20, 0, 8), (20, 1, 4), (50, 0, 8), (33, 0, 2), (40, 0, 8), (64, 0, 1)])
 def test_transr_parallel_fixed(dim, distance, St, mfma, monkeypatch):
     """Fixed (zeroed) energy; tiles of St samples (several per hot relation); the
     matrix-core kernels and the VALU ones.  St must not exceed the engine's own
