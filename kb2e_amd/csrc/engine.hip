@@ -1309,10 +1309,14 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
         }
 #endif
         if (getenv("KB2E_RPAR_STATS")) {  // transRNorm rounds of the PARALLEL TransR schedule
-            unsigned long long st[8];
+            unsigned long long st[16];
             HIPCHK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_rpar_rounds), sizeof(st)));
             fprintf(stderr, "rpar_rounds rounds of row blocks %llu, tiles with violators %llu, most rounds of a block %llu\n",
                     st[0], st[1], st[2]);
+            fprintf(stderr, "rpar_cons cycles: setup %llu, P0+rounds %llu, records %llu, longest block %llu, blocks %llu\n",
+                    st[3], st[4], st[5], st[6], st[7]);
+            fprintf(stderr, "rpar_rounds wave 0: loads+mfma issue %llu, barriers %llu, update part %llu, lockstep rounds %llu, "
+                    "tail %llu, G+ballot %llu\n", st[8], st[9], st[10], st[11], st[12], st[13]);
             std::memset(st, 0, sizeof(st));
             HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_rpar_rounds), st, sizeof(st)));
         }

@@ -39,7 +39,8 @@ struct Mfma16<float> {
     static __device__ __forceinline__ int row(int l, int r) { return 4 * (l >> 4) + r; }
 };
 
-// C = A B over 16 x 16 output tiles (MT x NT of them) and K (multiple of 4),
+// C = A B over 16 x 16 output tiles (MT x NT of them) and K (multiple of 4; rm_k4(n)
+// for a contraction over the n columns of an NP-padded image),
 // tiles dealt to the waves of the block; put(m, n, v) receives every element.
 // The fragments of eight k-steps are read from LDS before their MFMAs issue,
 // so the LDS latency is paid once per eight steps, not once per step.
@@ -61,7 +62,8 @@ __device__ __forceinline__ void block_gemm(int MT, int NT, int K, FA A, FB B, FP
                 bv[s] = ok ? B(k, bc) : T(0);
             }
 #pragma unroll
-            for (int s = 0; s < 8; ++s) acc = M::mma(av[s], bv[s], acc);
+            for (int s = 0; s < 8; ++s)
+                if (kb + 4 * s < K) acc = M::mma(av[s], bv[s], acc);  // no MFMA on the zero padding
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) put(mb * 16 + M::row(l, r), bc, acc[r]);
@@ -71,6 +73,7 @@ __device__ __forceinline__ void block_gemm(int MT, int NT, int K, FA A, FB B, FP
 __host__ __device__ constexpr int rm_np(int n) { return (n + 15) & ~15; }
 __host__ __device__ constexpr int rm_ld(int n) { return rm_np(n) + 2; }
 __host__ __device__ constexpr int rm_up16(int v) { return (v + 15) & ~15; }
+__host__ __device__ constexpr int rm_k4(int n) { return (n + 3) & ~3; }
 
 // Tile kernel LDS (elements of T): W [NP][L] | V [MV][L] | P [MV][L] | X [UY][L] | D [UY][L] | coef [UY] |
 // int ids [MV], kk [St]
@@ -82,12 +85,12 @@ __host__ __device__ constexpr size_t rmfma_tile_lds(int n, int St) {
 }
 
 // transRNorm kernel LDS: W [NP][L] | K [NP][L] | A0 [PP][L] | PG [PP][L] | s0 [PP] |
-// int ent_of, slot_of, rowmap, posmap, vio [PP] | 4
+// int ent_of, slot_of, rowmap, posmap, vio [PP] | 8 | npart [PP][NP / 16] | int vrow [PP]
 template <typename T>
 __host__ __device__ constexpr size_t rmfma_cons_lds(int n, int St) {
     return sizeof(T) * (2 * (size_t)rm_np(n) * rm_ld(n) + 2 * (size_t)rm_up16(4 * St + 1) * rm_ld(n) +
-                        rm_up16(4 * St + 1)) +
-           sizeof(int) * (5 * (size_t)rm_up16(4 * St + 1) + 4);
+                        (1 + (rm_np(n) <= 64 ? 4 : 8)) * (size_t)rm_up16(4 * St + 1)) +
+           sizeof(int) * (6 * (size_t)rm_up16(4 * St + 1) + 8);
 }
 
 template <typename T>
@@ -184,7 +187,7 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
     }
     __syncthreads();
     if (PROJ) {
-        block_gemm<T>(MV / 16, NP / 16, NP, [&](int m, int k) { return V[m * L + k]; },
+        block_gemm<T>(MV / 16, NP / 16, rm_k4(n), [&](int m, int k) { return V[m * L + k]; },
                       [&](int k, int c) { return Wl[k * L + c]; }, [&](int m, int c, T v) { P[m * L + c] = v; });
         __syncthreads();
         // one wave per sample: energies, hinge, x, d (transr/trainer.cpp:147-164, transr/transr.cpp:26-35)
@@ -254,7 +257,7 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
         }
         __syncthreads();
         // y = W x for every update (transr/trainer.cpp:168-169): Y = X W^T
-        block_gemm<T>(UY / 16, NP / 16, NP, [&](int m, int k) { return X[m * L + k]; },
+        block_gemm<T>(UY / 16, NP / 16, rm_k4(n), [&](int m, int k) { return X[m * L + k]; },
                       [&](int k, int c) { return Wl[c * L + k]; }, [&](int m, int c, T v) {
                           if (m < 2 * cnt && c < n) bf.y[((int64_t)kks[m >> 1] * 2 + (m & 1)) * ld + c] = v;
                       });
@@ -313,7 +316,7 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
 //   (MFMA), a flag per update slot (bf.pflag: the record is valid) and the
 //   tile's violator count (bf.cons_tile: 0 = no partial).
 // transRNorm statistics (tools): rounds summed over row blocks, tiles with violators, most rounds of a block
-__device__ unsigned long long g_rpar_rounds[8];
+__device__ unsigned long long g_rpar_rounds[16];
 
 // kConsNB: column blocks of 16 held in registers (NP / 16 <= kConsNB)
 template <typename T, int kConsNB>
@@ -337,9 +340,12 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
     int* rowmap = slot_of + PP;  // compacted row -> pq
     int* posmap = rowmap + PP;   // pq -> compacted row or -1
     int* vio = posmap + PP;      // compacted row violates (its pair moves)
-    int* misc = vio + PP;        // [0] live rows, [1] violators
+    int* misc = vio + PP;  // [0] live rows, [1] violators, [2 + 3 (m & 1) + b] row block b live at round m
+    T* npart = (T*)(misc + 8);   // [PP][kConsNB]: |p|^2 of a row over one column block
+    int* vrow = (int*)(npart + kConsNB * PP);  // the violators' rows, compacted: the rounds' row blocks
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = lane_id();
     const RTile tl = a.tiles[t];
+    const unsigned long long ck0 = bf.stats ? clock64() : 0ull;
     bool relpair = false;
     if (tl.q == 0) {
         int any = 0;
@@ -347,7 +353,11 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
         relpair = any != 0 && r < a.ne;
     }
     const int npairs = 4 * cnt + (relpair ? 1 : 0);
-    for (int pq = threadIdx.x; pq < PP; pq += blockDim.x) {
+    if (threadIdx.x == 0) misc[1] = 0;
+    if (w == 0) {
+        // the pairs, then the first occurrence of each entity compacted in pair
+        // order (PP <= kWave: one lane per pair) while the other waves stage W
+        const int pq = l;
         int ent = -1, slot = -1;
         if (pq < 4 * cnt) {
             const int q = pq >> 2, u = (pq >> 1) & 1, role = pq & 1;
@@ -364,33 +374,31 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
             ent = r;  // entityVec_next_[relation] (transr/trainer.cpp:187)
             slot = -2;
         }
-        ent_of[pq] = ent;
-        slot_of[pq] = slot;
-        vio[pq] = 0;
-    }
-    stage_matrix_padded(Wl, bf.W + (int64_t)r * n * ld, n, ld);
-    if (threadIdx.x == 0) misc[1] = 0;
-    __syncthreads();
-    if (w == 0) {  // first occurrence of each entity, compacted in pair order
-        int base = 0;
-        for (int p0 = 0; p0 < PP; p0 += kWave) {
-            const int pq = p0 + l;
-            const int ent = pq < PP ? ent_of[pq] : -1;
-            bool dup = false;
-            const int kmax = min(PP, p0 + kWave);  // PP is a multiple of 16
-            for (int k = 0; k < kmax; k += 4) {
-                const int4 e4 = *(const int4*)(ent_of + k);
-                dup |= (k < pq && e4.x == ent) | (k + 1 < pq && e4.y == ent) | (k + 2 < pq && e4.z == ent) |
-                       (k + 3 < pq && e4.w == ent);
-            }
-            const bool live = ent >= 0 && !dup;
-            const uint64_t m = __ballot(live);
-            const int pos = base + __builtin_popcountll(m & ((1ull << l) - 1));
-            if (live) rowmap[pos] = pq;
-            if (pq < PP) posmap[pq] = live ? pos : -1;
-            base += __builtin_popcountll(m);
+        if (pq < PP) {
+            ent_of[pq] = ent;
+            slot_of[pq] = slot;
+            vio[pq] = 0;
         }
-        if (l == 0) misc[0] = base;
+        wave_lds_sync();
+        bool dup = false;
+        for (int k = 0; k < PP; k += 4) {  // PP is a multiple of 16
+            const int4 e4 = *(const int4*)(ent_of + k);
+            dup |= (k < pq && e4.x == ent) | (k + 1 < pq && e4.y == ent) | (k + 2 < pq && e4.z == ent) |
+                   (k + 3 < pq && e4.w == ent);
+        }
+        const bool live = ent >= 0 && !dup;
+        const uint64_t m = __ballot(live);
+        const int pos = __builtin_popcountll(m & ((1ull << l) - 1));
+        if (live) rowmap[pos] = pq;
+        if (pq < PP) posmap[pq] = live ? pos : -1;
+        if (l == 0) misc[0] = __builtin_popcountll(m);
+    } else {
+        const T* Wg = bf.W + (int64_t)r * n * ld;
+#pragma unroll 8
+        for (int idx = threadIdx.x - kWave; idx < NP * L; idx += blockDim.x - kWave) {
+            const int j = idx / L, i = idx % L;
+            Wl[idx] = (j < n && i < n) ? Wg[(int64_t)j * ld + i] : T(0);
+        }
     }
     __syncthreads();
     const int nrows = misc[0];
@@ -401,9 +409,81 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
         A0[idx] = (e >= 0 && i < n) ? bf.ent[(int64_t)e * ld + i] : T(0);
     }
     __syncthreads();
-    if (nrows > 0) {
+    const unsigned long long ck1 = bf.stats ? clock64() : 0ull;
+    const T lr = (T)a.lr;
+    // One wave per 16-row block (MR / 16 <= PP / 16 <= the block's waves):
+    // P0 = A0 W0 and the check; only a tile with violators goes on to
+    // K = W0^T W0, s0 = a0.a0 and the rounds.
+    const int mb = w;
+    const bool rows_here = mb < MR / 16;
+    const int ar = mb * 16 + (l & 15), kq = l >> 4;
+    typename M::acc_t pf[kConsNB];
+    T nrm[4];
+    bool live[4];
+    auto rowsq = [&](T (&nr)[4]) {  // |p|^2 of the lane's four rows
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nr[q] = T(0);
+#pragma unroll
+        for (int nb = 0; nb < kConsNB; ++nb) {
+            if (nb >= NB) break;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                T v = pf[nb][q] * pf[nb][q];
+                v += dpp_ror<8>(v);
+                v += dpp_ror<4>(v);
+                v += dpp_ror<2>(v);
+                v += dpp_ror<1>(v);
+                nr[q] += v;
+            }
+        }
+    };
+    // rows of Aop (this block) x Bop over k < rm_k4(n) (past it the images are zero)
+    const int K4 = rm_k4(n);
+    auto mul = [&](const T* Aop, const T* Bop, typename M::acc_t (&out)[kConsNB]) {
+#pragma unroll
+        for (int nb = 0; nb < kConsNB; ++nb) {
+            if (nb >= NB) break;
+            typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
+            const int bc = nb * 16 + (l & 15);
+            for (int kb = 0; kb < K4; kb += 32) {
+                T av[8], bv[8];
+#pragma unroll
+                for (int s8 = 0; s8 < 8; ++s8) {
+                    const int k = kb + 4 * s8 + kq;
+                    const bool ok = kb + 4 * s8 < K4;
+                    av[s8] = ok ? Aop[ar * L + k] : T(0);
+                    bv[s8] = ok ? Bop[k * L + bc] : T(0);
+                }
+#pragma unroll
+                for (int s8 = 0; s8 < 8; ++s8)
+                    if (kb + 4 * s8 < K4) acc = M::mma(av[s8], bv[s8], acc);
+            }
+            out[nb] = acc;
+        }
+    };
+    if (rows_here) {
+        mul(A0, Wl, pf);
+        rowsq(nrm);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) live[q] = mb * 16 + M::row(l, q) < nrows && nrm[q] > T(1);
+        if ((l & 15) == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (live[q]) vio[mb * 16 + M::row(l, q)] = 1;
+        }
+        const uint64_t anyv = __ballot(live[0] || live[1] || live[2] || live[3]);  // all lanes take part
+        if (l == 0 && anyv) atomicAdd(&misc[1], 1);
+#pragma unroll
+        for (int nb = 0; nb < kConsNB; ++nb) {
+            if (nb >= NB) break;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) PG[(mb * 16 + M::row(l, q)) * L + nb * 16 + (l & 15)] = pf[nb][q];
+        }
+    }
+    __syncthreads();
+    if (misc[1] != 0) {
         // K = W0^T W0 (symmetric, zero past n) and s0 = a0.a0
-        block_gemm<T>(NB, NB, NP, [&](int m, int k) { return Wl[k * L + m]; },
+        block_gemm<T>(NB, NB, rm_k4(n), [&](int m, int k) { return Wl[k * L + m]; },
                       [&](int k, int c) { return Wl[k * L + c]; }, [&](int m, int c, T v) { K[m * L + c] = v; });
         for (int row = w; row < nrows; row += nw) {
             T ss = T(0);
@@ -411,110 +491,163 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
             ss = wave_sum(ss);
             if (l == 0) s0[row] = ss;
         }
-    }
-    __syncthreads();
-    const T lr = (T)a.lr;
-    // one wave per 16-row block: P0 = A0 W0, then the rounds on its violators
-    for (int mb = w; mb < MR / 16; mb += nw) {
-        typename M::acc_t pf[kConsNB], gf[kConsNB];
-        const int ar = mb * 16 + (l & 15), kq = l >> 4;
-        auto rowsq = [&](T (&nrm)[4]) {  // |p|^2 of the lane's four rows
+        if (w == 0) {  // MR <= PP <= kWave
+            const bool v = l < MR && vio[l] != 0;
+            const uint64_t vm = __ballot(v);
+            if (v) vrow[__builtin_popcountll(vm & ((1ull << l) - 1))] = l;
+            if (l == 0) {
+                const int nv = __builtin_popcountll(vm);
+                misc[0] = nv;
+                for (int b = 0; b < 3; ++b) misc[2 + b] = b * 16 < nv;  // every violator is live at round 0
+            }
+        }
+        __syncthreads();
+        const int nviol = misc[0];
+        // The rounds on the violators' rows only (vrow: 16-row blocks of
+        // them, usually one), all blocks in lockstep, one (row block, column
+        // block) task per wave: a task keeps its 16 x 16 slice of p and G in
+        // registers; PG holds the whole p of every row; |p|^2 is summed over
+        // the column blocks' partials in column order.  A frozen row (its
+        // first non-violation) keeps p, so it stays at <= 1, and a block with
+        // no live row skips its MFMAs.
+        constexpr int kTasks = (3 * kConsNB + 7) / 8;  // 3 row blocks x NB column blocks over 8 waves
+        const int ntask = (rm_up16(nviol) / 16) * NB;
+        auto vr_row = [&](int vr) { return vr < nviol ? vrow[vr] : -1; };
+        typename M::acc_t ps[kTasks], gs[kTasks];
+        bool lv[kTasks][4];
+        T cs[kTasks][4];
+        int rounds[kTasks] = {};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) nrm[q] = T(0);
+        for (int i = 0; i < kTasks; ++i) {
+            const int task = w + i * nw;
+            const int tm = task / NB, tn = task % NB;
 #pragma unroll
-            for (int nb = 0; nb < kConsNB; ++nb) {
-                if (nb >= NB) break;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    T v = pf[nb][q] * pf[nb][q];
-                    v += dpp_ror<8>(v);
-                    v += dpp_ror<4>(v);
-                    v += dpp_ror<2>(v);
-                    v += dpp_ror<1>(v);
-                    nrm[q] += v;
-                }
+            for (int q = 0; q < 4; ++q) {
+                const int row = task < ntask ? vr_row(tm * 16 + M::row(l, q)) : -1;
+                ps[i][q] = row >= 0 ? PG[row * L + tn * 16 + (l & 15)] : T(0);
+                gs[i][q] = T(0);
+                lv[i][q] = row >= 0;
+                cs[i][q] = row >= 0 ? T(2) * lr * s0[row] : T(0);
+            }
+        }
+        unsigned long long ckr[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
+        unsigned long long ckp = bf.stats ? clock64() : 0ull;
+        auto rmark = [&](int k) {
+            if (bf.stats) {
+                const unsigned long long c = clock64();
+                ckr[k] += c - ckp;
+                ckp = c;
             }
         };
-        auto mul = [&](const T* Aop, const T* Bop, typename M::acc_t (&out)[kConsNB]) {  // rows of Aop (this block) x Bop
+        for (int m = 0; m < kRParMaxIter; ++m) {
+            typename M::acc_t qs[kTasks];
+            rmark(4);
 #pragma unroll
-            for (int nb = 0; nb < kConsNB; ++nb) {
-                if (nb >= NB) break;
+            for (int i = 0; i < kTasks; ++i) {
+                const int task = w + i * nw;
+                if (task >= ntask) break;
+                const int tm = task / NB, tn = task % NB;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (lv[i][q]) gs[i][q] += T(2) * ps[i][q];
+                const uint64_t busy = __ballot(lv[i][0] || lv[i][1] || lv[i][2] || lv[i][3]);
+                if (busy) ++rounds[i];
+                if (i == 0) rmark(5);
+                // (K p) for this slice: rows tm of P times columns tn of K
                 typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
-                const int bc = nb * 16 + (l & 15);
-                for (int kb = 0; kb < NP; kb += 32) {
+                const int ar2 = vr_row(tm * 16 + (l & 15)), bc = tn * 16 + (l & 15);
+                for (int kb = 0; busy && kb < K4; kb += 32) {
                     T av[8], bv[8];
 #pragma unroll
                     for (int s8 = 0; s8 < 8; ++s8) {
                         const int k = kb + 4 * s8 + kq;
-                        const bool ok = kb + 4 * s8 < NP;
-                        av[s8] = ok ? Aop[ar * L + k] : T(0);
-                        bv[s8] = ok ? Bop[k * L + bc] : T(0);
+                        const bool ok = kb + 4 * s8 < K4;
+                        av[s8] = ok && ar2 >= 0 ? PG[ar2 * L + k] : T(0);
+                        bv[s8] = ok ? K[k * L + bc] : T(0);
                     }
 #pragma unroll
-                    for (int s8 = 0; s8 < 8; ++s8) acc = M::mma(av[s8], bv[s8], acc);
+                    for (int s8 = 0; s8 < 8; ++s8)
+                        if (kb + 4 * s8 < K4) acc = M::mma(av[s8], bv[s8], acc);
                 }
-                out[nb] = acc;
+                qs[i] = acc;
             }
-        };
-        mul(A0, Wl, pf);
-        T nrm[4], cc[4];
-        bool live[4];
-        rowsq(nrm);
+            rmark(0);
+            __syncthreads();  // P read by every task; the row blocks' live flags for round m complete
+            rmark(1);
+            const int* fl = misc + 2 + 3 * (m & 1);
+            if ((fl[0] | fl[1] | fl[2]) == 0) break;
+            ckr[3] += 1;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int row = mb * 16 + M::row(l, q);
-            live[q] = row < nrows && nrm[q] > T(1);
-            cc[q] = row < nrows ? T(2) * lr * s0[row] : T(0);
-        }
-#pragma unroll
-        for (int nb = 0; nb < kConsNB; ++nb) gf[nb] = {T(0), T(0), T(0), T(0)};
-        if ((l & 15) == 0) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (live[q]) vio[mb * 16 + M::row(l, q)] = 1;
-        }
-        int m = 0;
-        for (; m < kRParMaxIter; ++m) {
-            if (!__ballot(live[0] || live[1] || live[2] || live[3])) break;
-#pragma unroll
-            for (int nb = 0; nb < kConsNB; ++nb) {
-                if (nb >= NB) break;
+            for (int i = 0; i < kTasks; ++i) {
+                const int task = w + i * nw;
+                if (task >= ntask) break;
+                const int tm = task / NB, tn = task % NB;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    if (live[q]) gf[nb][q] += T(2) * pf[nb][q];
-                    PG[(mb * 16 + M::row(l, q)) * L + nb * 16 + (l & 15)] = pf[nb][q];
+                    const int vr = tm * 16 + M::row(l, q), row = vr_row(vr);
+                    ps[i][q] = lv[i][q] ? ps[i][q] - T(2) * lr * qs[i][q] - cs[i][q] * ps[i][q] : ps[i][q];
+                    if (row >= 0) PG[row * L + tn * 16 + (l & 15)] = ps[i][q];
+                    T v = ps[i][q] * ps[i][q];
+                    v += dpp_ror<8>(v);
+                    v += dpp_ror<4>(v);
+                    v += dpp_ror<2>(v);
+                    v += dpp_ror<1>(v);
+                    if ((l & 15) == 0) npart[vr * kConsNB + tn] = v;
                 }
             }
-            typename M::acc_t qf[kConsNB];
-            wave_lds_sync();
-            mul(PG, K, qf);  // K p
-            wave_lds_sync();
+            rmark(2);
+            __syncthreads();  // P and the partial norms of this round
+            rmark(1);
 #pragma unroll
-            for (int nb = 0; nb < kConsNB; ++nb) {
-                if (nb >= NB) break;
+            for (int i = 0; i < kTasks; ++i) {
+                const int task = w + i * nw;
+                if (task >= ntask) break;
+                const int tm = task / NB, tn = task % NB;
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    pf[nb][q] = live[q] ? pf[nb][q] - T(2) * lr * qf[nb][q] - cc[q] * pf[nb][q] : pf[nb][q];
+                for (int q = 0; q < 4; ++q) {
+                    const int vr = tm * 16 + M::row(l, q);
+                    T pp[kConsNB];
+#pragma unroll
+                    for (int c = 0; c < kConsNB; ++c) pp[c] = c < NB ? npart[vr * kConsNB + c] : T(0);
+                    T nr = T(0);
+#pragma unroll
+                    for (int c = 0; c < kConsNB; ++c)
+                        if (c < NB) nr += pp[c];
+                    lv[i][q] = lv[i][q] && nr > T(1);
+                }
+                const uint64_t any = __ballot(lv[i][0] || lv[i][1] || lv[i][2] || lv[i][3]);
+                if (tn == 0 && l == 0) misc[2 + 3 * ((m + 1) & 1) + tm] = any != 0;
             }
-            rowsq(nrm);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) live[q] = live[q] && nrm[q] > T(1);
         }
+        // G replaces P (every read of P is behind the last barrier): the
+        // violators' slices, zeros on the other rows
 #pragma unroll
-        for (int nb = 0; nb < kConsNB; ++nb) {
-            if (nb >= NB) break;
+        for (int i = 0; i < kTasks; ++i) {
+            const int task = w + i * nw;
+            if (task >= ntask) break;
+            const int tm = task / NB, tn = task % NB;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) PG[(mb * 16 + M::row(l, q)) * L + nb * 16 + (l & 15)] = gf[nb][q];
+            for (int q = 0; q < 4; ++q) {
+                const int row = vr_row(tm * 16 + M::row(l, q));
+                if (row >= 0) PG[row * L + tn * 16 + (l & 15)] = gs[i][q];
+            }
         }
-        if (l == 0 && m > 0) {
-            atomicAdd(&misc[1], 1);
-            if (bf.stats) {
-                atomicAdd(&g_rpar_rounds[0], (unsigned long long)m);
-                atomicMax(&g_rpar_rounds[2], (unsigned long long)m);
+        for (int idx = threadIdx.x; idx < MR * L; idx += blockDim.x)
+            if (!vio[idx / L]) PG[idx] = T(0);
+        if (bf.stats && threadIdx.x == 0)
+            for (int k = 0; k < 6; ++k) atomicAdd(&g_rpar_rounds[8 + k], ckr[k]);
+        if (bf.stats) {
+            for (int i = 0; i < kTasks; ++i) {
+                const int task = w + i * nw;
+                if (task < ntask && task % NB == 0 && l == 0 && rounds[i] > 0) {
+                    atomicAdd(&g_rpar_rounds[0], (unsigned long long)rounds[i]);
+                    atomicMax(&g_rpar_rounds[2], (unsigned long long)rounds[i]);
+                }
             }
         }
     }
     __syncthreads();
+    const unsigned long long ck2 = bf.stats ? clock64() : 0ull;
     if (w == 0) {  // pair flags and the tile's entry
         for (int pq = l; pq < 4 * cnt; pq += kWave) {
             const int slot = slot_of[pq];
@@ -527,9 +660,17 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
             if (misc[1] && bf.stats) atomicAdd(&g_rpar_rounds[1], 1ull);
         }
     }
-    if (misc[1] == 0) return;
+    if (misc[1] == 0) {
+        if (bf.stats && threadIdx.x == 0) {
+            atomicAdd(&g_rpar_rounds[3], ck1 - ck0);
+            atomicAdd(&g_rpar_rounds[4], ck2 - ck1);
+            atomicMax(&g_rpar_rounds[6], clock64() - ck0);
+            atomicAdd(&g_rpar_rounds[7], 1ull);
+        }
+        return;
+    }
     // pair records da = -lr W0 G (B(k, c) = W0[c][k])
-    block_gemm<T>(MR / 16, NB, NP, [&](int m, int k) { return PG[m * L + k]; },
+    block_gemm<T>(MR / 16, NB, rm_k4(n), [&](int m, int k) { return PG[m * L + k]; },
                   [&](int k, int c) { return Wl[c * L + k]; }, [&](int m, int c, T v) {
                       if (m >= nrows || c >= n || !vio[m]) return;
                       const int sl = slot_of[rowmap[m]];
@@ -544,6 +685,17 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
                   [&](int j, int i, T v) {
                       if (j < n && i < n) wp[(int64_t)j * ld + i] = -lr * v;
                   });
+    if (bf.stats) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned long long ck3 = clock64();
+            atomicAdd(&g_rpar_rounds[3], ck1 - ck0);
+            atomicAdd(&g_rpar_rounds[4], ck2 - ck1);
+            atomicAdd(&g_rpar_rounds[5], ck3 - ck2);
+            atomicMax(&g_rpar_rounds[6], ck3 - ck0);
+            atomicAdd(&g_rpar_rounds[7], 1ull);
+        }
+    }
 }
 
 }  // namespace kb2e
