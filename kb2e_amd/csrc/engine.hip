@@ -167,7 +167,7 @@ struct kb2e_ctx {
     // PARALLEL schedule: per-event records in sorted order (kernels_transe.hpp EventRecs)
     DevBuf ev_iota, ev_slot_sorted, ev_inv, seg_row, ev_meta, ev_words;
     // PARALLEL TransR (kernels_transr_parallel.hpp)
-    int32_t rpar_St = 8, rpar_max_tiles = 1;
+    int32_t rpar_St = 8, rpar_max_tiles = 1, rpar_tile_threads = 256;
     bool rpar_no_constraint = false;
     bool rpar_mfma = false;  // matrix-core tile kernels (kernels_transr_mfma.hpp)
     DevBuf rpar_pflag, rpar_cons_tile;

@@ -75,21 +75,22 @@ __host__ __device__ constexpr int rm_ld(int n) { return rm_np(n) + 2; }
 __host__ __device__ constexpr int rm_up16(int v) { return (v + 15) & ~15; }
 __host__ __device__ constexpr int rm_k4(int n) { return (n + 3) & ~3; }
 
-// Tile kernel LDS (elements of T): W [NP][L] | V [MV][L] | P [MV][L] | X [UY][L] | D [UY][L] | coef [UY] |
-// int ids [MV], kk [St]
+// Tile kernel LDS (elements of T): W [NP][L] | V [MV][L] | P [MV][L] (PROJ) | X [UY][L] | D [UY][L] |
+// coef [UY] (GRAD) | int ids [MV], kk [St].  A projection-only launch needs no D, a
+// gradient-only one (compat) neither W, V nor P: smaller images, more workgroups per CU.
 template <typename T>
-__host__ __device__ constexpr size_t rmfma_tile_lds(int n, int St) {
-    return sizeof(T) * ((size_t)rm_np(n) * rm_ld(n) + 2 * (size_t)rm_up16(4 * St) * rm_ld(n) +
-                        2 * (size_t)rm_up16(2 * St) * rm_ld(n) + rm_up16(2 * St)) +
+__host__ __device__ constexpr size_t rmfma_tile_lds(int n, int St, bool proj = true, bool grad = true) {
+    return sizeof(T) * ((proj ? (size_t)rm_np(n) * rm_ld(n) + 2 * (size_t)rm_up16(4 * St) * rm_ld(n) : 0) +
+                        (grad ? 2 : 1) * (size_t)rm_up16(2 * St) * rm_ld(n) + rm_up16(2 * St)) +
            sizeof(int) * ((size_t)rm_up16(4 * St) + St);
 }
 
-// transRNorm kernel LDS: W [NP][L] | K [NP][L] | A0 [PP][L] | PG [PP][L] | s0 [PP] |
+// transRNorm kernel LDS: W [NP][L] | K [NP][L] | A0 [PP][L] | PG [PP + 1][L] | s0 [PP + 2] |
 // int ent_of, slot_of, rowmap, posmap, vio [PP] | 8 | npart [PP][NP / 16] | int vrow [PP]
 template <typename T>
 __host__ __device__ constexpr size_t rmfma_cons_lds(int n, int St) {
-    return sizeof(T) * (2 * (size_t)rm_np(n) * rm_ld(n) + 2 * (size_t)rm_up16(4 * St + 1) * rm_ld(n) +
-                        (1 + (rm_np(n) <= 64 ? 4 : 8)) * (size_t)rm_up16(4 * St + 1)) +
+    return sizeof(T) * (2 * (size_t)rm_np(n) * rm_ld(n) + (2 * (size_t)rm_up16(4 * St + 1) + 1) * rm_ld(n) + 2 +
+                        (1 + rm_np(n) / 16) * (size_t)rm_up16(4 * St + 1)) +
            sizeof(int) * (6 * (size_t)rm_up16(4 * St + 1) + 8);
 }
 
@@ -154,11 +155,11 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
     const int n = a.n, ld = a.ld, NP = rm_np(n), L = rm_ld(n);
     const int MV = rm_up16(4 * a.St), UY = rm_up16(2 * a.St);
     T* Wl = (T*)smem;
-    T* V = Wl + NP * L;
-    T* P = V + MV * L;
-    T* X = P + MV * L;
-    T* D = X + UY * L;
-    T* coef = D + UY * L;
+    T* V = Wl + (PROJ ? NP * L : 0);
+    T* P = V + (PROJ ? MV * L : 0);
+    T* X = P + (PROJ ? MV * L : 0);
+    T* D = X + UY * L;  // GRAD only
+    T* coef = D + (GRAD ? UY * L : 0);
     int* ids = (int*)(coef + UY);  // entity of every V row
     int* kks = ids + MV;           // sample index of every tile sample
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = lane_id();
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
     if (PROJ) stage_matrix_padded(Wl, bf.W + (int64_t)r * n * ld, n, ld);
     for (int idx = threadIdx.x; idx < UY * L; idx += blockDim.x) {
         X[idx] = T(0);
-        D[idx] = T(0);
+        if (GRAD) D[idx] = T(0);
     }
     for (int idx = threadIdx.x; idx < UY; idx += blockDim.x) coef[idx] = T(0);
     __syncthreads();
@@ -318,7 +319,8 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
 // transRNorm statistics (tools): rounds summed over row blocks, tiles with violators, most rounds of a block
 __device__ unsigned long long g_rpar_rounds[16];
 
-// kConsNB: column blocks of 16 held in registers (NP / 16 <= kConsNB)
+// kConsNB: the column blocks of 16, exactly (NP = 16 kConsNB): every loop over
+// them and over the k-steps below NP has a compile-time trip count.
 template <typename T, int kConsNB>
 __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParBufs<T> bf) {
     using M = Mfma16<T>;
@@ -328,14 +330,15 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
     if (t >= a.tile_first[a.batch_seg[a.batch + 1]]) return;
     int r, e0, cnt;
     tile_range(a, t, r, e0, cnt);
-    const int n = a.n, ld = a.ld, NP = rm_np(n), L = rm_ld(n), NB = NP / 16;
+    constexpr int NB = kConsNB, NP = 16 * NB, L = NP + 2;
+    const int n = a.n, ld = a.ld;
     const int PP = rm_up16(4 * a.St + 1);
     T* Wl = (T*)smem;
     T* K = Wl + NP * L;
     T* A0 = K + NP * L;
-    T* PG = A0 + PP * L;  // P during the rounds, then G
-    T* s0 = PG + PP * L;
-    int* ent_of = (int*)(s0 + PP);
+    T* PG = A0 + PP * L;  // P during the rounds, then G; row PP: zeros (the rounds' padding rows)
+    T* s0 = PG + (PP + 1) * L;  // [PP + 1], s0[PP] = 0
+    int* ent_of = (int*)(s0 + PP + 1 + 1);
     int* slot_of = ent_of + PP;  // pair slot (kk * 2 + u) * 2 + role, -2 for (entity[r], r), -1 none
     int* rowmap = slot_of + PP;  // compacted row -> pq
     int* posmap = rowmap + PP;   // pq -> compacted row or -1
@@ -393,6 +396,10 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
         if (pq < PP) posmap[pq] = live ? pos : -1;
         if (l == 0) misc[0] = __builtin_popcountll(m);
     } else {
+        if (w == 1) {  // the zero row of PG and s0[PP]
+            for (int i = l; i < L; i += kWave) PG[PP * L + i] = T(0);
+            if (l == 0) s0[PP] = T(0);
+        }
         const T* Wg = bf.W + (int64_t)r * n * ld;
 #pragma unroll 8
         for (int idx = threadIdx.x - kWave; idx < NP * L; idx += blockDim.x - kWave) {
@@ -445,12 +452,13 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
             if (nb >= NB) break;
             typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
             const int bc = nb * 16 + (l & 15);
-            for (int kb = 0; kb < K4; kb += 32) {
+#pragma unroll
+            for (int kb = 0; kb < NP; kb += 32) {
                 T av[8], bv[8];
 #pragma unroll
                 for (int s8 = 0; s8 < 8; ++s8) {
                     const int k = kb + 4 * s8 + kq;
-                    const bool ok = kb + 4 * s8 < K4;
+                    const bool ok = kb + 4 * s8 < NP;  // compile time; zeros past n in the images
                     av[s8] = ok ? Aop[ar * L + k] : T(0);
                     bv[s8] = ok ? Bop[k * L + bc] : T(0);
                 }
@@ -512,7 +520,7 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
         // no live row skips its MFMAs.
         constexpr int kTasks = (3 * kConsNB + 7) / 8;  // 3 row blocks x NB column blocks over 8 waves
         const int ntask = (rm_up16(nviol) / 16) * NB;
-        auto vr_row = [&](int vr) { return vr < nviol ? vrow[vr] : -1; };
+        auto vr_row = [&](int vr) { return vr < nviol ? vrow[vr] : PP; };  // PP: the zero row
         typename M::acc_t ps[kTasks], gs[kTasks];
         bool lv[kTasks][4];
         T cs[kTasks][4];
@@ -523,11 +531,11 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
             const int tm = task / NB, tn = task % NB;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int row = task < ntask ? vr_row(tm * 16 + M::row(l, q)) : -1;
-                ps[i][q] = row >= 0 ? PG[row * L + tn * 16 + (l & 15)] : T(0);
+                const int row = task < ntask ? vr_row(tm * 16 + M::row(l, q)) : PP;
+                ps[i][q] = PG[row * L + tn * 16 + (l & 15)];
                 gs[i][q] = T(0);
-                lv[i][q] = row >= 0;
-                cs[i][q] = row >= 0 ? T(2) * lr * s0[row] : T(0);
+                lv[i][q] = row < PP;
+                cs[i][q] = T(2) * lr * s0[row];
             }
         }
         unsigned long long ckr[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
@@ -556,13 +564,15 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
                 // (K p) for this slice: rows tm of P times columns tn of K
                 typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
                 const int ar2 = vr_row(tm * 16 + (l & 15)), bc = tn * 16 + (l & 15);
-                for (int kb = 0; busy && kb < K4; kb += 32) {
+#pragma unroll
+                for (int kb = 0; kb < NP; kb += 32) {
+                    if (!busy) break;
                     T av[8], bv[8];
 #pragma unroll
                     for (int s8 = 0; s8 < 8; ++s8) {
                         const int k = kb + 4 * s8 + kq;
-                        const bool ok = kb + 4 * s8 < K4;
-                        av[s8] = ok && ar2 >= 0 ? PG[ar2 * L + k] : T(0);
+                        const bool ok = kb + 4 * s8 < NP;  // compile time
+                        av[s8] = ok ? PG[ar2 * L + k] : T(0);
                         bv[s8] = ok ? K[k * L + bc] : T(0);
                     }
 #pragma unroll
@@ -586,13 +596,13 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
                 for (int q = 0; q < 4; ++q) {
                     const int vr = tm * 16 + M::row(l, q), row = vr_row(vr);
                     ps[i][q] = lv[i][q] ? ps[i][q] - T(2) * lr * qs[i][q] - cs[i][q] * ps[i][q] : ps[i][q];
-                    if (row >= 0) PG[row * L + tn * 16 + (l & 15)] = ps[i][q];
+                    PG[row * L + tn * 16 + (l & 15)] = ps[i][q];  // the zero row stays zero
                     T v = ps[i][q] * ps[i][q];
                     v += dpp_ror<8>(v);
                     v += dpp_ror<4>(v);
                     v += dpp_ror<2>(v);
                     v += dpp_ror<1>(v);
-                    if ((l & 15) == 0) npart[vr * kConsNB + tn] = v;
+                    if ((l & 15) == 0) npart[vr * NB + tn] = v;
                 }
             }
             rmark(2);
@@ -608,11 +618,10 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
                     const int vr = tm * 16 + M::row(l, q);
                     T pp[kConsNB];
 #pragma unroll
-                    for (int c = 0; c < kConsNB; ++c) pp[c] = c < NB ? npart[vr * kConsNB + c] : T(0);
+                    for (int c = 0; c < NB; ++c) pp[c] = npart[vr * NB + c];
                     T nr = T(0);
 #pragma unroll
-                    for (int c = 0; c < kConsNB; ++c)
-                        if (c < NB) nr += pp[c];
+                    for (int c = 0; c < NB; ++c) nr += pp[c];
                     lv[i][q] = lv[i][q] && nr > T(1);
                 }
                 const uint64_t any = __ballot(lv[i][0] || lv[i][1] || lv[i][2] || lv[i][3]);
@@ -628,8 +637,7 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
             const int tm = task / NB, tn = task % NB;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int row = vr_row(tm * 16 + M::row(l, q));
-                if (row >= 0) PG[row * L + tn * 16 + (l & 15)] = gs[i][q];
+                PG[vr_row(tm * 16 + M::row(l, q)) * L + tn * 16 + (l & 15)] = gs[i][q];
             }
         }
         for (int idx = threadIdx.x; idx < MR * L; idx += blockDim.x)

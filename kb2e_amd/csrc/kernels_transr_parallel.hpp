@@ -343,27 +343,40 @@ __global__ __launch_bounds__(256) void transr_rel_rows_kernel(RParArgs a, RParBu
     // an active update; matrix-core transRNorm step: only tiles whose pairs moved
     // have a partial
     const bool sel = !NORM && bf.cons_tile;
-    int any = 0;
-    for (int t = t0; t < t1; ++t) any |= sel ? bf.cons_tile[t - tb] : a.tile_act[t];
+    // the tiles that carry a partial, 64 flags per load (lane-parallel, not a
+    // serial scan: a hot relation has tens of tiles)
+    auto flags = [&](int base) {
+        const int t = base + lane_id();
+        const int f = t < t1 ? (sel ? bf.cons_tile[t - tb] : a.tile_act[t]) : 0;
+        return (uint64_t)__ballot(f != 0);
+    };
+    uint64_t any = 0;
+    for (int base = t0; base < t1 && !any; base += kWave) any = flags(base);
     if (!any) return;
     T* row = j < n ? bf.W + ((int64_t)r * n + j) * ld : bf.rel + (int64_t)r * ld;
     T v[2];
     lane_pair_load(row, n, v);
-    for (int t = t0; t < t1; t += 4) {  // four partial rows in flight, summed in tile order
-        T p[4][2];
-        bool use[4];
+    for (int base = t0; base < t1; base += kWave) {
+        // every tile's partial (the VALU transRNorm step writes one for each
+        // tile), or only the flagged ones of the matrix-core transRNorm step
+        uint64_t m = sel ? flags(base) : (uint64_t)__ballot(base + lane_id() < t1);
+        while (m) {  // eight partial rows in flight, summed in tile order
+            T p[8][2];
+            bool use[8];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t lt = t + q - tb;
-            use[q] = t + q < t1 && (!sel || bf.cons_tile[lt] != 0);
-            if (use[q]) lane_pair_load(j < n ? bf.wpart + (lt * n + j) * ld : bf.rpart + lt * ld, n, p[q]);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (use[q]) {
-                v[0] += p[q][0];
-                v[1] += p[q][1];
+            for (int q = 0; q < 8; ++q) {
+                use[q] = m != 0;
+                const int64_t lt = use[q] ? base + __builtin_ctzll(m) - tb : 0;
+                m &= m - 1;
+                if (use[q]) lane_pair_load(j < n ? bf.wpart + (lt * n + j) * ld : bf.rpart + lt * ld, n, p[q]);
             }
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (use[q]) {
+                    v[0] += p[q][0];
+                    v[1] += p[q][1];
+                }
+        }
     }
     if (NORM) {
         const T len = sqrt(wave_sum(v[0] * v[0] + v[1] * v[1]));
