@@ -619,13 +619,23 @@ template <typename T, bool GRAD>
 __global__ __launch_bounds__(1024) void transr_entity_kernel(RParArgs a, RParBufs<T> bf, int32_t long_min) {
     __shared__ T part[kRParWaves][2][kWave];
     __shared__ int flags[2];
+    __shared__ int longs[1024], nlong;
     const int w = threadIdx.x >> 6, l = lane_id();
     const int s0 = a.batch_seg[a.batch], s1 = a.rel_begin[a.batch];  // entity segments sort first
     const int G = gridDim.x;
-    // long segments: whole workgroup, segments s0 + blockIdx.x, s0 + blockIdx.x + G, ... that are long
-    for (int s = s0 + blockIdx.x; s < s1; s += G) {
+    // long segments: whole workgroup, segments s0 + blockIdx.x, s0 + blockIdx.x + G, ... that are
+    // long, found by one thread each (blockDim.x candidates per pass; the order between
+    // segments is immaterial, each is a different row)
+    for (int c0 = s0 + blockIdx.x; c0 < s1; c0 += G * (int)blockDim.x) {
+        if (threadIdx.x == 0) nlong = 0;
+        __syncthreads();
+        const int cs = c0 + G * (int)threadIdx.x;
+        if (cs < s1 && a.seg_start[cs + 1] - a.seg_start[cs] >= long_min) longs[atomicAdd(&nlong, 1)] = cs;
+        __syncthreads();
+        const int nl = nlong;
+        for (int li = 0; li < nl; ++li) {
+        const int s = longs[li];
         const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
-        if (p1 - p0 < long_min) continue;
         const int row = a.seg_row[s];
         if (threadIdx.x < 2) flags[threadIdx.x] = 0;
         __syncthreads();
@@ -647,6 +657,7 @@ __global__ __launch_bounds__(1024) void transr_entity_kernel(RParArgs a, RParBuf
             rpar_entity_finish<T, GRAD>(a, bf, row, acc, flags[0] != 0, flags[1] != 0);
         }
         __syncthreads();
+        }
     }
     // short segments: one wave each
     for (int s = s0 + blockIdx.x * kRParWaves + w; s < s1; s += G * kRParWaves) {
