@@ -47,11 +47,13 @@ struct HParArgs {
     uint8_t* orth_mask;       // [B] violating (update, row) pairs of each sample, bits u * 3 + {r, h, t}
 };
 
-// One 1024-thread workgroup per relation segment of the batch: waves sum
-// chunks of its events, partial sums combined in wave order, wave 0 applies.
-template <typename T, int CH>
-__global__ __launch_bounds__(1024) void transh_w_apply_kernel(HParArgs<T> a) {
-    __shared__ T part[16][CH * kVec][kWave];
+// One NWV-wave workgroup per relation segment of the batch: waves sum chunks
+// of its events, partial sums combined in wave order, wave 0 applies.  The
+// hottest relation (~1100 events on FB15k-shaped batches) sets the time, so
+// the default is 16 waves (8 and 4 measured 16% and 50% slower).
+template <typename T, int CH, int NWV>
+__global__ __launch_bounds__(NWV * kWave) void transh_w_apply_kernel(HParArgs<T> a) {
+    __shared__ T part[NWV][CH * kVec][kWave];
     __shared__ int any;
     const int s = a.rel_begin[a.batch] + blockIdx.x;
     if (s >= a.batch_seg[a.batch + 1]) return;
@@ -62,7 +64,7 @@ __global__ __launch_bounds__(1024) void transh_w_apply_kernel(HParArgs<T> a) {
     __syncthreads();
     T acc[CH][kVec] = {};
     bool act_any = false;
-    for (int base = p0 + w * kWave; base < p1; base += 16 * kWave) {
+    for (int base = p0 + w * kWave; base < p1; base += NWV * kWave) {
         const int p = base + l;
         int xrow = -1;
         if (p < p1) {
@@ -133,7 +135,7 @@ __global__ __launch_bounds__(1024) void transh_w_apply_kernel(HParArgs<T> a) {
 #pragma unroll
         for (int k = 0; k < kVec; ++k) {
             T sum = part[0][cc * kVec + k][l];
-            for (int v = 1; v < 16; ++v) sum += part[v][cc * kVec + k][l];
+            for (int v = 1; v < NWV; ++v) sum += part[v][cc * kVec + k][l];
             if (elem_valid(cc, k, a.n)) W.v[cc][k] = W.v[cc][k] + sum;
         }
     W.norm(a.n, false);
@@ -175,41 +177,81 @@ __global__ __launch_bounds__(256) void transh_orth_check_kernel(HParArgs<T> a) {
 }
 
 // One wave, samples in order: the reference's normOrth (common/utils.cpp:79-111,
-// orth_norm) on every flagged pair, in place on the live rows.
+// orth_norm) on every flagged pair, in place on the live rows.  Per pass the
+// flag words of 2048 samples are loaded at once and the flagged samples listed
+// in sample order in LDS; their ids (r, h, t, h', t') are fetched for 64 list
+// entries at a time, so the serial part is only the rows' load / normOrth /
+// store.  w_r stays in registers across the flagged rows of one sample (the
+// reference reloads what it just stored).
+constexpr int kOrthWords = 4;  // 8-byte flag words per lane per pass
+
 template <typename T, int CH>
 __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
+    __shared__ int list[8 * kWave * kOrthWords];
     const int l = lane_id();
-    // eight samples' flags per lane (orth_mask is zero past B up to a multiple of 512)
-    for (int base = 0; base < a.B; base += 8 * kWave) {
-        const uint64_t word = *reinterpret_cast<const uint64_t*>(a.orth_mask + base + 8 * l);
-        uint64_t m = __ballot(word != 0ull);
-        while (m) {
-            const int e = __builtin_ctzll(m);
-            m &= m - 1;
-            const uint64_t wd = readlane_u64(word, e);
-            for (int by = 0; by < 8; ++by) {
-                const uint32_t bits = (uint32_t)((wd >> (8 * by)) & 0xffu);
-                if (!bits) continue;
-                const int k2 = base + 8 * e + by;
+    for (int base = 0; base < a.B; base += 8 * kWave * kOrthWords) {
+        uint64_t word[kOrthWords];
+#pragma unroll
+        for (int wi = 0; wi < kOrthWords; ++wi) {  // orth_mask is zero past B up to a multiple of 512
+            const int off = base + 8 * (wi * kWave + l);
+            word[wi] = off < a.B ? *reinterpret_cast<const uint64_t*>(a.orth_mask + off) : 0ull;
+        }
+        int count = 0;
+#pragma unroll
+        for (int wi = 0; wi < kOrthWords; ++wi) {  // sample order: word, lane, byte
+            int mine = 0;
+#pragma unroll
+            for (int by = 0; by < 8; ++by) mine += ((word[wi] >> (8 * by)) & 0xffu) != 0;
+            int pre = mine;  // inclusive scan over the lanes
+#pragma unroll
+            for (int d = 1; d < kWave; d <<= 1) {
+                const int v = __shfl_up(pre, d);
+                if (l >= d) pre += v;
+            }
+            int pos = count + pre - mine;
+#pragma unroll
+            for (int by = 0; by < 8; ++by)
+                if (((word[wi] >> (8 * by)) & 0xffu) != 0) list[pos++] = base + 8 * (wi * kWave + l) + by;
+            count += __shfl(pre, kWave - 1);
+        }
+        wave_lds_sync();
+        for (int g = 0; g < count; g += kWave) {
+            int k2 = -1, r = 0, h = 0, t = 0, nh = 0, nt = 0, bits = 0;
+            if (g + l < count) {  // this lane's list entry: ids from the sample stream
+                k2 = list[g + l];
                 const int i0 = a.si[k2], j = a.sj[k2];
-                const int h = a.heads[i0], t = a.tails[i0], r = a.rels[i0];
-                const int nh = a.side[k2] ? h : j, nt = a.side[k2] ? j : t;
-                T* rows[6] = {a.rel + (int64_t)r * a.ld, a.ent + (int64_t)h * a.ld, a.ent + (int64_t)t * a.ld,
-                              a.rel + (int64_t)r * a.ld, a.ent + (int64_t)nh * a.ld, a.ent + (int64_t)nt * a.ld};
-                T* wrow = a.w + (int64_t)r * a.ld;
+                const bool sd = a.side[k2];
+                bits = a.orth_mask[k2];
+                h = a.heads[i0];
+                t = a.tails[i0];
+                r = a.rels[i0];
+                nh = sd ? h : j;
+                nt = sd ? j : t;
+            }
+            const int ng = min(kWave, count - g);
+            for (int e = 0; e < ng; ++e) {
+                const uint32_t eb = (uint32_t)readlane_i32(bits, e);
+                const int er = readlane_i32(r, e);
+                const int ids[6] = {er, readlane_i32(h, e), readlane_i32(t, e), er, readlane_i32(nh, e),
+                                    readlane_i32(nt, e)};
+                T* wrow = a.w + (int64_t)er * a.ld;
+                RowReg<T, CH> W;
+                row_load_sc1(W, wrow, a.n);
                 for (int q = 0; q < 6; ++q) {
-                    if (!((bits >> q) & 1u)) continue;
+                    if (!((eb >> q) & 1u)) continue;
+                    T* row = (q == 0 || q == 3 ? a.rel : a.ent) + (int64_t)ids[q] * a.ld;
                     // agent-scope (L1-bypassing) accesses: a later pair may reload a row stored here
-                    RowReg<T, CH> A, W;
-                    row_load_sc1(A, rows[q], a.n);
-                    row_load_sc1(W, wrow, a.n);
+                    RowReg<T, CH> A;
+                    row_load_sc1(A, row, a.n);
                     orth_norm<T, CH>(A, W, a.n, (T)a.lr);
-                    row_store_sc1(A, rows[q], a.n);
-                    row_store_sc1(W, wrow, a.n);
+                    row_store_sc1(A, row, a.n);
                     drain_stores();
                 }
+                row_store_sc1(W, wrow, a.n);
+                drain_stores();
             }
         }
+        wave_lds_sync();
     }
 }
 

@@ -174,3 +174,4 @@ def test_transh_parallel(dim):
 
 def test_transh_parallel_small():
     _transh_vs_model(data.synthetic("small", seed=1), 64, 2, batches=20, rate=0.001)
+
