@@ -203,7 +203,8 @@ struct HScoreArgs {
     double* loss;
     uint64_t* xbits;  // [B][2][nw]
     T* scal;          // [B][2][4]: headSum, tailSum, sum_x
-    T* snap;          // [B][2][2][ld]: snapshot head row, tail row
+    T* snap;          // [B][2][2][ld]: snapshot head row, tail row; EMIT: [B][2][ld] w deltas
+    double lr;        // EMIT: the w deltas' beta lr
 };
 
 // transh/transh.cpp:10-29 energies, transh/trainer.cpp:14-33 directions.
@@ -297,6 +298,23 @@ __global__ __launch_bounds__(256) void transh_score_kernel(HScoreArgs<T> a, Even
         T* s1 = a.scal + ((int64_t)kk * 2 + 1) * 4;
         s0[0] = hs_p; s0[1] = ts_p; s0[2] = sx_p;
         s1[0] = hs_n; s1[1] = ts_n; s1[2] = sx_n;
+    }
+    if (EMIT) {
+        // PARALLEL: each update's w delta  beta lr ((hs - ts) x + sum_x (h - t))
+        // (transh/trainer.cpp:39-46), the expression transh_w_apply_kernel sums
+        const T cp = (T)(-1.0 * a.lr), cn = (T)(1.0 * a.lr);
+        RowReg<T, CH> Dp, Dn;
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) {
+                const T xp = dp[c][k] > T(0) ? T(1) : T(-1), xn = dn[c][k] > T(0) ? T(1) : T(-1);
+                Dp.v[c][k] = cp * ((hs_p - ts_p) * xp + sx_p * (H.v[c][k] - Tt.v[c][k]));
+                Dn.v[c][k] = cn * ((hs_n - ts_n) * xn + sx_n * (NH.v[c][k] - NT.v[c][k]));
+            }
+        Dp.store(a.snap + ((int64_t)kk * 2 + 0) * a.ld, a.n);
+        Dn.store(a.snap + ((int64_t)kk * 2 + 1) * a.ld, a.n);
+        return;
     }
     H.store(a.snap + (((int64_t)kk * 2 + 0) * 2 + 0) * a.ld, a.n);
     Tt.store(a.snap + (((int64_t)kk * 2 + 0) * 2 + 1) * a.ld, a.n);

@@ -40,7 +40,7 @@ struct HParArgs {
     const int32_t* meta;      // event records (kernels_transe.hpp EventRecs)
     const uint64_t* words;
     const T* scal;            // [B][2][4] hs, ts, sum_x
-    const T* snap;            // [B][2][2][ld] snapshot head, tail rows
+    const T* snap;            // [B][2][ld] each update's w delta (transh_score_kernel, EMIT)
     T* ent;
     T* rel;
     T* w;
@@ -73,8 +73,8 @@ __global__ __launch_bounds__(NWV * kWave) void transh_w_apply_kernel(HParArgs<T>
         }
         uint64_t m = __ballot(xrow >= 0);
         if (m) act_any = true;
-        while (m) {  // eight updates at a time: their loads in flight together
-            constexpr int G = 8;
+        while (m) {  // G updates' delta rows (score kernel) in flight together, summed in event order
+            constexpr int G = 16 / CH;
             int ev[G], xr[G];
             int ne4 = 0;
             for (; ne4 < G && m; ++ne4) {
@@ -82,41 +82,27 @@ __global__ __launch_bounds__(NWV * kWave) void transh_w_apply_kernel(HParArgs<T>
                 m &= m - 1;
                 xr[ne4] = readlane_i32(xrow, ev[ne4]);
             }
-            T hs[G], ts[G], sx[G], hv[G][CH][kVec], tv[G][CH][kVec];
-            uint64_t words[G][2 * CH];
+            T dv[G][CH][kVec];
 #pragma unroll
             for (int q = 0; q < G; ++q) {
                 if (q >= ne4) continue;
-                const T* sc = a.scal + (int64_t)xr[q] * 4;
-                hs[q] = sc[0];
-                ts[q] = sc[1];
-                sx[q] = sc[2];
-                const T* hrow = a.snap + ((int64_t)xr[q] * 2 + 0) * a.ld;
-                const T* trow = a.snap + ((int64_t)xr[q] * 2 + 1) * a.ld;
+                const T* drow = a.snap + (int64_t)xr[q] * a.ld;
 #pragma unroll
                 for (int cc = 0; cc < CH; ++cc)
 #pragma unroll
                     for (int k = 0; k < kVec; ++k) {
                         const int el = cc * (kWave * kVec) + l * kVec + k;
-                        hv[q][cc][k] = el < a.n ? hrow[el] : T(0);
-                        tv[q][cc][k] = el < a.n ? trow[el] : T(0);
+                        dv[q][cc][k] = el < a.n ? drow[el] : T(0);
                     }
-#pragma unroll
-                for (int wq = 0; wq < 2 * CH; ++wq)
-                    words[q][wq] = wq < a.nw ? a.words[(int64_t)(base + ev[q]) * a.nw + wq] : 0ull;
             }
 #pragma unroll
             for (int q = 0; q < G; ++q) {
                 if (q >= ne4) continue;
-                const T c = (T)(((xr[q] & 1) ? 1.0 : -1.0) * a.lr);  // beta lr
 #pragma unroll
                 for (int cc = 0; cc < CH; ++cc)
 #pragma unroll
-                    for (int k = 0; k < kVec; ++k) {
-                        if (!elem_valid(cc, k, a.n)) continue;
-                        const T x = xbit(words[q], cc, k) ? T(1) : T(-1);
-                        acc[cc][k] += c * ((hs[q] - ts[q]) * x + sx[q] * (hv[q][cc][k] - tv[q][cc][k]));
-                    }
+                    for (int k = 0; k < kVec; ++k)
+                        if (elem_valid(cc, k, a.n)) acc[cc][k] += dv[q][cc][k];
             }
         }
     }
