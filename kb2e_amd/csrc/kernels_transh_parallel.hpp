@@ -167,14 +167,39 @@ __global__ __launch_bounds__(256) void transh_orth_check_kernel(HParArgs<T> a) {
 // flag words of 2048 samples are loaded at once and the flagged samples listed
 // in sample order in LDS; their ids (r, h, t, h', t') are fetched for 64 list
 // entries at a time, so the serial part is only the rows' load / normOrth /
-// store.  w_r stays in registers across the flagged rows of one sample (the
-// reference reloads what it just stored).
+// store.  w_r stays in registers while consecutive flagged samples share the
+// relation (the reference reloads what it just stored), and a store is drained
+// only before a later load of the same row (PendingRows).
 constexpr int kOrthWords = 4;  // 8-byte flag words per lane per pass
+
+// Rows stored by this wave and not yet drained: a load of one of them waits
+// for the stores first (s_waitcnt vmcnt(0)); everything else loads at once.
+struct PendingRows {
+    static constexpr int kCap = 8;
+    int id[kCap];
+    int cnt = 0;
+    __device__ void drain() {
+        drain_stores();
+        cnt = 0;
+    }
+    __device__ void before_load(int key) {
+        bool hit = false;
+        for (int i = 0; i < cnt; ++i) hit |= id[i] == key;
+        if (hit) drain();
+    }
+    __device__ void add(int key) {
+        if (cnt == kCap) drain();
+        id[cnt++] = key;
+    }
+};
 
 template <typename T, int CH>
 __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
     __shared__ int list[8 * kWave * kOrthWords];
     const int l = lane_id();
+    RowReg<T, CH> W;
+    int wid = -1;
+    PendingRows pend;
     for (int base = 0; base < a.B; base += 8 * kWave * kOrthWords) {
         uint64_t word[kOrthWords];
 #pragma unroll
@@ -220,25 +245,34 @@ __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
                 const int er = readlane_i32(r, e);
                 const int ids[6] = {er, readlane_i32(h, e), readlane_i32(t, e), er, readlane_i32(nh, e),
                                     readlane_i32(nt, e)};
-                T* wrow = a.w + (int64_t)er * a.ld;
-                RowReg<T, CH> W;
-                row_load_sc1(W, wrow, a.n);
+                if (er != wid) {  // w_r: kept in registers while consecutive samples share the relation
+                    if (wid >= 0) {
+                        row_store_sc1(W, a.w + (int64_t)wid * a.ld, a.n);
+                        pend.add(a.nr + wid);
+                    }
+                    pend.before_load(a.nr + er);
+                    row_load_sc1(W, a.w + (int64_t)er * a.ld, a.n);
+                    wid = er;
+                }
                 for (int q = 0; q < 6; ++q) {
                     if (!((eb >> q) & 1u)) continue;
-                    T* row = (q == 0 || q == 3 ? a.rel : a.ent) + (int64_t)ids[q] * a.ld;
-                    // agent-scope (L1-bypassing) accesses: a later pair may reload a row stored here
+                    const bool isrel = q == 0 || q == 3;
+                    T* row = (isrel ? a.rel : a.ent) + (int64_t)ids[q] * a.ld;
+                    // ids: relations [0, nr), w rows [nr, 2 nr), entities from 2 nr
+                    const int key = isrel ? ids[q] : 2 * a.nr + ids[q];
                     RowReg<T, CH> A;
+                    pend.before_load(key);
                     row_load_sc1(A, row, a.n);
                     orth_norm<T, CH>(A, W, a.n, (T)a.lr);
                     row_store_sc1(A, row, a.n);
-                    drain_stores();
+                    pend.add(key);
                 }
-                row_store_sc1(W, wrow, a.n);
-                drain_stores();
             }
         }
         wave_lds_sync();
     }
+    if (wid >= 0) row_store_sc1(W, a.w + (int64_t)wid * a.ld, a.n);
+    drain_stores();
 }
 
 }  // namespace kb2e
