@@ -256,8 +256,11 @@ def main():
         import torch.distributed as dist
         import torch
 
+        # test knobs (tests/test_gpu_distributed.py): every rank on device 0, gloo
+        if os.environ.get("KB2E_DIST_ONE_DEVICE"):
+            local = 0
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("KB2E_DIST_BACKEND", "nccl"))
 
     model, shape, dim, method, distance, rate = CONFIGS[args.config]
     ds = data.synthetic(shape, seed=0)
