@@ -44,6 +44,9 @@ CONFIGS = {
     "transh_fb15k": ("H", "fb15k", 100, 1, 0, 0.001),
     "transr_fb15k": ("R", "fb15k", 50, 1, 0, 0.001),
     "transe_wn18": ("E", "wn18", 50, 0, 0, 0.001),
+    # BASELINE configs[4]: 1M entities, 10k relations, 16M triples;
+    # tables drawn by numpy (the reference's host randn init takes minutes at this size)
+    "transr_k5": ("R", "k5", 100, 1, 0, 0.001),
 }
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 
@@ -145,9 +148,20 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup):
                  batches=batches, seed=7 + rank, precision=args.precision, device=local if world > 1 else 0,
                  schedule=schedule)
     eng.upload_triples(train)
-    ent, rel, w = eng.init_params()
-    if model == "R":
-        eng.transr_seed(ent, rel)  # seed = the init draws (no TransE run in the bench)
+    if shape == "k5":
+        import numpy as np
+
+        rng = np.random.default_rng(7)
+        ent = rng.uniform(-1, 1, (ds.num_entities, dim))
+        ent /= np.linalg.norm(ent, axis=1, keepdims=True)
+        rel = rng.uniform(-1, 1, (ds.num_relations, dim))
+        rel /= np.linalg.norm(rel, axis=1, keepdims=True)
+        w = np.broadcast_to(np.eye(dim), (ds.num_relations, dim, dim)).reshape(eng.wshape())  # identity Mr
+        eng.upload_params(ent, rel, np.ascontiguousarray(w))
+    else:
+        ent, rel, w = eng.init_params()
+        if model == "R":
+            eng.transr_seed(ent, rel)  # seed = the init draws (no TransE run in the bench)
     B = len(train) // batches
     merger = None
     if world > 1:
@@ -263,7 +277,7 @@ def main():
         dist.init_process_group(os.environ.get("KB2E_DIST_BACKEND", "nccl"))
 
     model, shape, dim, method, distance, rate = CONFIGS[args.config]
-    ds = data.synthetic(shape, seed=0)
+    ds = data.synthetic(shape, seed=1 if shape == "k5" else 0)
     train = shard_heads(ds.train, rank, world) if world > 1 else ds.train
     main_run = measure(args, args.schedule, ds, train, rank, world, local, dist, args.steps, args.warmup)
     other = "ordered" if args.schedule == "parallel" else "parallel"
@@ -288,7 +302,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64" if args.precision == 64 else "f32",
-        "data": f"synthetic {shape}-shaped (kb2e_amd.data.synthetic, seed 0), reference glibc sample stream seed 7",
+        "data": f"synthetic {shape}-shaped (kb2e_amd.data.synthetic, seed {1 if shape == 'k5' else 0}), reference "
+                f"glibc sample stream seed 7" + (", numpy-drawn unit-row tables, identity Mr" if shape == "k5" else ""),
         "config": {"workload": f"{args.config}: {'TransE' if model == 'E' else 'TransH' if model == 'H' else 'TransR'} "
                                f"n={dim} {'bern' if method else 'unif'} L{distance + 1}, {batches} batches of {B} "
                                f"per GPU, {args.schedule} schedule",
