@@ -7,7 +7,9 @@
 // class below keeps the shape of common::Trainer (common/trainer.h:14-78):
 // add / loadFiles / train / write, with prepTrain and bfgs as the overridable
 // steps -- and bfgs() runs on the GPU through include/kb2e_engine.h.
-// GPU-only flags are additive: --precision 64|32, --device N, --transrcompat 0|1.
+// GPU-only flags are additive: --precision 64|32, --device N, --transrcompat 0|1,
+// --schedule 0|1 (0 = ORDERED, the reference's sequence; 1 = PARALLEL, summed
+// per-row deltas with one norm per batch, kb2e_engine.h kb2e_schedule).
 #include <sys/stat.h>
 
 #include <cmath>
@@ -47,6 +49,7 @@ struct EmbeddingArguments {  // common/args.h:9-25, defaults common/constants.h:
     int precision = 64;
     int device = 0;
     int transrCompat = 1;
+    int schedule = 0;
 
     std::string to_string() const {  // common/args.cpp:33-50
         std::string r = "Options: [";
@@ -100,6 +103,7 @@ void printUsage(const char* invoked) {  // common/args.cpp:125-142
     printf("   --precision [64] (GPU: 64 or 32)\n");
     printf("   --device [0] (GPU ordinal)\n");
     printf("   --transrcompat [1] (TransR: reproduce the accumulating energy)\n");
+    printf("   --schedule [0] (GPU: 0 ordered = the reference's sequence, 1 parallel)\n");
 }
 
 EmbeddingArguments parseArgs(int argc, char** argv) {  // common/args.cpp:53-122
@@ -124,6 +128,7 @@ EmbeddingArguments parseArgs(int argc, char** argv) {  // common/args.cpp:53-122
     if ((i = argpos("precision", true, argc, argv)) != -1) a.precision = atoi(argv[i + 1]);
     if ((i = argpos("device", true, argc, argv)) != -1) a.device = atoi(argv[i + 1]);
     if ((i = argpos("transrcompat", true, argc, argv)) != -1) a.transrCompat = atoi(argv[i + 1]);
+    if ((i = argpos("schedule", true, argc, argv)) != -1) a.schedule = atoi(argv[i + 1]) ? 1 : 0;
     return a;
 }
 
@@ -271,6 +276,7 @@ class Trainer {  // the interface of common::Trainer (common/trainer.h:14-78)
         cfg.precision = args_.precision;
         cfg.device = args_.device;
         cfg.transr_compat = args_.transrCompat;
+        cfg.schedule = args_.schedule ? KB2E_SCHEDULE_PARALLEL : KB2E_SCHEDULE_ORDERED;
         check(nullptr, kb2e_create(&cfg, &ctx_), "create");
         check(ctx_, kb2e_upload_triples(ctx_, heads_.data(), tails_.data(), relations_.data(), (int64_t)heads_.size()),
               "upload_triples");

@@ -84,3 +84,21 @@ def test_eval_cli_matches_reference_eval(tmp_path):
     ev = run["eval"]
     assert lines["Raw"] == "Raw      -- Rank: %f, Hits@10: %f" % (ev["raw"]["rank"], ev["raw"]["hits10"])
     assert lines["Filtered"] == "Filtered -- Rank: %f, Hits@10: %f" % (ev["filtered"]["rank"], ev["filtered"]["hits10"])
+
+
+@pytest.mark.parametrize("prog,name", [("trainTransE", "transe_l1_bern"), ("trainTransH", "transh_bern")])
+def test_train_cli_parallel_schedule(tmp_path, prog, name):
+    """--schedule 1: the PARALLEL schedule behind the same CLI and file formats.
+    Same epoch count and file shapes; losses close to the reference's (the
+    schedule differs from it at O(lr^2) per row with several updates a batch)."""
+    stdout, out, run = _run(tmp_path, prog, name, ["--schedule", "1"])
+    ref = open(os.path.join(GOLDEN, name, "stdout.txt")).read()
+    mine, theirs = _epoch_lines(stdout), _epoch_lines(ref)
+    assert len(mine) == len(theirs)
+    lm = np.array([float(l.split("Loss:")[1]) for l in mine])
+    lr = np.array([float(l.split("Loss:")[1]) for l in theirs])
+    assert np.all(np.abs(lm - lr) <= 0.05 * np.abs(lr) + 1.0)
+    for f in ["entity2vec.bern", "relation2vec.bern"]:
+        a = np.array(open(out / f).read().split(), dtype=np.float64)
+        b = np.array(open(os.path.join(GOLDEN, name, f)).read().split(), dtype=np.float64)
+        assert a.shape == b.shape and np.isfinite(a).all()
