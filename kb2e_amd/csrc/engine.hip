@@ -11,6 +11,7 @@
 //      relation-owner schedule for TransH/TransR) -- the reference's
 //      prebatch/postbatch snapshot semantics without any table copies.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -263,6 +264,34 @@ struct kb2e_ctx {
         HIPCHK(hipEventRecord(b, st));
         pending.push_back({name, a, b});
         if (pending.size() > 4096) flush_timers();
+    }
+
+    // Kernel-timestamp timing (hipExtLaunchKernelGGL): the start / stop events
+    // are taken at the kernel's own start and end, not around its dispatch, so
+    // the averages match rocprofv3's kernel durations.  ev_begin() gives the
+    // start event of a span (first kernel) and ev_end() its stop event (last
+    // kernel); both null when this batch is not sampled.
+    hipEvent_t span_a = nullptr;
+    const char* span_name = nullptr;
+    void ev_begin(const char* name, hipEvent_t& a) {
+        a = nullptr;
+        if (!prof || !prof_batch) return;
+        a = span_a = get_event();
+        span_name = name;
+    }
+    void ev_end(hipEvent_t& b) {
+        b = nullptr;
+        if (!span_a) return;
+        b = get_event();
+        pending.push_back({span_name, span_a, b});
+        span_a = nullptr;
+    }
+    template <typename... KArgs, typename... Args>
+    void launch(void (*kernel)(KArgs...), dim3 grid, dim3 block, size_t lds, hipEvent_t a, hipEvent_t b,
+                Args... args) {
+        if (a || b) hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, a, b, 0, args...);
+        else hipLaunchKernelGGL(kernel, grid, block, lds, stream, args...);
+        HIPCHK(hipGetLastError());
     }
 
     void flush_timers() {
@@ -683,11 +712,11 @@ void run_batch_transe_parallel(kb2e_ctx* c, int64_t b) {
     const bool l1 = c->cfg.distance == 0;
     const int grid = (int)((c->B + 3) / 4);
     const EventRecs er = event_recs(c);
-    c->timed("score", [&] {
-        if (l1) transe_score_kernel<T, CH, true, true><<<grid, 256, 0, c->stream>>>(sa, er, c->kl, b * c->B);
-        else transe_score_kernel<T, CH, false, true><<<grid, 256, 0, c->stream>>>(sa, er, c->kl, b * c->B);
-        HIPCHK(hipGetLastError());
-    });
+    hipEvent_t e0, e1;
+    c->ev_begin("score", e0);
+    c->ev_end(e1);
+    if (l1) c->launch(transe_score_kernel<T, CH, true, true>, dim3(grid), dim3(256), 0, e0, e1, sa, er, c->kl, b * c->B);
+    else c->launch(transe_score_kernel<T, CH, false, true>, dim3(grid), dim3(256), 0, e0, e1, sa, er, c->kl, b * c->B);
     FoldArgs<T> fa{};
     fa.keys = c->keys_sorted.as<uint64_t>();
     fa.seg_start = c->seg_start.as<int32_t>();
@@ -706,15 +735,18 @@ void run_batch_transe_parallel(kb2e_ctx* c, int64_t b) {
     fa.xreal = sa.xreal;
     fa.gram_min = 0;
     fa.long_min = c->apply_long_min;
-    c->timed("apply", [&] {  // phase B is this one kernel
-        if (l1)
-            transe_apply_kernel<T, CH, true><<<c->apply_grid, 1024, 0, c->stream>>>(
-                fa, er, c->par_long_list.as<int32_t>(), c->par_long_count.as<int32_t>(), c->par_long_cap);
-        else
-            transe_apply_kernel<T, CH, false><<<c->apply_grid, 1024, 0, c->stream>>>(
-                fa, er, c->par_long_list.as<int32_t>(), c->par_long_count.as<int32_t>(), c->par_long_cap);
-        HIPCHK(hipGetLastError());
-    });
+    // phase B is this one kernel
+    c->ev_begin("apply", e0);
+    c->ev_end(e1);
+    const int32_t* ll = c->par_long_list.as<int32_t>();
+    const int32_t* lc = c->par_long_count.as<int32_t>();
+    if (l1)
+        c->launch(transe_apply_kernel<T, CH, true>, dim3(c->apply_grid), dim3(1024), 0, e0, e1, fa, er, ll, lc,
+                  c->par_long_cap);
+    else
+        c->launch(transe_apply_kernel<T, CH, false>, dim3(c->apply_grid), dim3(1024), 0, e0, e1, fa, er, ll, lc,
+                  c->par_long_cap);
+    if (c->pending.size() > 4096) c->flush_timers();
 }
 
 template <typename K>

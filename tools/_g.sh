@@ -1,5 +1,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/t
-timeout -k 10 300 python -u -m pytest tests/test_gpu_cli.py -x -v --timeout 120 --timeout-method thread > gpurun_out/t/cli.log 2>&1 || { echo "tests failed"; grep -E "^E |Error|assert" gpurun_out/t/cli.log | head -30; exit 1; }
-tail -3 gpurun_out/t/cli.log
+for c in transe_fb15k transr_fb15k; do
+timeout -k 10 120 python bench.py --config $c --steps 300 --warmup 100 --only --no-cpu-baseline > gpurun_out/t/b.json || exit 1
+python -c "import json; d=json.loads(open('gpurun_out/t/b.json').read().strip().splitlines()[-1]); print('$c', round(d['value']/1e6,2), d['roofline']['kernels_avg_us'], d['roofline']['frac'])"
+done
