@@ -525,17 +525,28 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
         bool lv[kTasks][4];
         T cs[kTasks][4];
         int rounds[kTasks] = {};
+        // loop invariants: each task's rows (A operand row of the lane, rows of
+        // its four results) and, for the first task, its K fragment
+        int arow[kTasks], orow[kTasks][4];
+        constexpr int KS = NB <= 4 ? NP / 4 : 1;  // k-steps of a cached K fragment
+        T kf[KS];
 #pragma unroll
         for (int i = 0; i < kTasks; ++i) {
             const int task = w + i * nw;
             const int tm = task / NB, tn = task % NB;
+            arow[i] = task < ntask ? vr_row(tm * 16 + (l & 15)) : PP;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int row = task < ntask ? vr_row(tm * 16 + M::row(l, q)) : PP;
+                orow[i][q] = row;
                 ps[i][q] = PG[row * L + tn * 16 + (l & 15)];
                 gs[i][q] = T(0);
                 lv[i][q] = row < PP;
                 cs[i][q] = T(2) * lr * s0[row];
+            }
+            if (i == 0 && NB <= 4) {
+#pragma unroll
+                for (int s4 = 0; s4 < KS; ++s4) kf[s4] = K[(4 * s4 + kq) * L + tn * 16 + (l & 15)];
             }
         }
         unsigned long long ckr[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
@@ -554,7 +565,7 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
             for (int i = 0; i < kTasks; ++i) {
                 const int task = w + i * nw;
                 if (task >= ntask) break;
-                const int tm = task / NB, tn = task % NB;
+                const int tn = task % NB;
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     if (lv[i][q]) gs[i][q] += T(2) * ps[i][q];
@@ -563,7 +574,7 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
                 if (i == 0) rmark(5);
                 // (K p) for this slice: rows tm of P times columns tn of K
                 typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
-                const int ar2 = vr_row(tm * 16 + (l & 15)), bc = tn * 16 + (l & 15);
+                const int ar2 = arow[i], bc = tn * 16 + (l & 15);
 #pragma unroll
                 for (int kb = 0; kb < NP; kb += 32) {
                     if (!busy) break;
@@ -573,7 +584,8 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
                         const int k = kb + 4 * s8 + kq;
                         const bool ok = kb + 4 * s8 < NP;  // compile time
                         av[s8] = ok ? PG[ar2 * L + k] : T(0);
-                        bv[s8] = ok ? K[k * L + bc] : T(0);
+                        if (i == 0 && NB <= 4) bv[s8] = ok ? kf[(kb / 4 + s8) % KS] : T(0);
+                        else bv[s8] = ok ? K[k * L + bc] : T(0);
                     }
 #pragma unroll
                     for (int s8 = 0; s8 < 8; ++s8)
@@ -594,7 +606,7 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
                 const int tm = task / NB, tn = task % NB;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const int vr = tm * 16 + M::row(l, q), row = vr_row(vr);
+                    const int vr = tm * 16 + M::row(l, q), row = orow[i][q];
                     ps[i][q] = lv[i][q] ? ps[i][q] - T(2) * lr * qs[i][q] - cs[i][q] * ps[i][q] : ps[i][q];
                     PG[row * L + tn * 16 + (l & 15)] = ps[i][q];  // the zero row stays zero
                     T v = ps[i][q] * ps[i][q];
@@ -634,10 +646,10 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
         for (int i = 0; i < kTasks; ++i) {
             const int task = w + i * nw;
             if (task >= ntask) break;
-            const int tm = task / NB, tn = task % NB;
+            const int tn = task % NB;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                PG[vr_row(tm * 16 + M::row(l, q)) * L + tn * 16 + (l & 15)] = gs[i][q];
+                PG[orow[i][q] * L + tn * 16 + (l & 15)] = gs[i][q];
             }
         }
         for (int idx = threadIdx.x; idx < MR * L; idx += blockDim.x)
