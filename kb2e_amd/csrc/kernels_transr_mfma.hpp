@@ -85,12 +85,12 @@ __host__ __device__ constexpr size_t rmfma_tile_lds(int n, int St, bool proj = t
            sizeof(int) * ((size_t)rm_up16(4 * St) + St);
 }
 
-// transRNorm kernel LDS: W [NP][L] | K [NP][L] | A0 [PP][L] | PG [PP + 1][L] | s0 [PP + 2] |
-// int ent_of, slot_of, rowmap, posmap, vio [PP] | 8 | npart [PP][NP / 16] | int vrow [PP]
+// transRNorm kernel LDS: W [NP][L] | K [NP][L] | A0 [PP][L] | PG, PG2 [PP + 1][L] | s0 [PP + 2] |
+// int ent_of, slot_of, rowmap, posmap, vio [PP] | 8 | npart [2][PP][NP / 16] | int vrow [PP]
 template <typename T>
 __host__ __device__ constexpr size_t rmfma_cons_lds(int n, int St) {
-    return sizeof(T) * (2 * (size_t)rm_np(n) * rm_ld(n) + (2 * (size_t)rm_up16(4 * St + 1) + 1) * rm_ld(n) + 2 +
-                        (1 + rm_np(n) / 16) * (size_t)rm_up16(4 * St + 1)) +
+    return sizeof(T) * (2 * (size_t)rm_np(n) * rm_ld(n) + (3 * (size_t)rm_up16(4 * St + 1) + 2) * rm_ld(n) + 2 +
+                        (1 + 2 * (rm_np(n) / 16)) * (size_t)rm_up16(4 * St + 1)) +
            sizeof(int) * (6 * (size_t)rm_up16(4 * St + 1) + 8);
 }
 
@@ -337,15 +337,16 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
     T* K = Wl + NP * L;
     T* A0 = K + NP * L;
     T* PG = A0 + PP * L;  // P during the rounds, then G; row PP: zeros (the rounds' padding rows)
-    T* s0 = PG + (PP + 1) * L;  // [PP + 1], s0[PP] = 0
+    T* PG2 = PG + (PP + 1) * L;  // the rounds' second P buffer, row PP zeros
+    T* s0 = PG2 + (PP + 1) * L;  // [PP + 1], s0[PP] = 0
     int* ent_of = (int*)(s0 + PP + 1 + 1);
     int* slot_of = ent_of + PP;  // pair slot (kk * 2 + u) * 2 + role, -2 for (entity[r], r), -1 none
     int* rowmap = slot_of + PP;  // compacted row -> pq
     int* posmap = rowmap + PP;   // pq -> compacted row or -1
     int* vio = posmap + PP;      // compacted row violates (its pair moves)
     int* misc = vio + PP;  // [0] live rows, [1] violators, [2 + 3 (m & 1) + b] row block b live at round m
-    T* npart = (T*)(misc + 8);   // [PP][kConsNB]: |p|^2 of a row over one column block
-    int* vrow = (int*)(npart + kConsNB * PP);  // the violators' rows, compacted: the rounds' row blocks
+    T* npart = (T*)(misc + 8);   // [2][PP][kConsNB]: |p|^2 of a row over one column block, per round parity
+    int* vrow = (int*)(npart + 2 * kConsNB * PP);  // the violators' rows, compacted: the rounds' row blocks
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = lane_id();
     const RTile tl = a.tiles[t];
     const unsigned long long ck0 = bf.stats ? clock64() : 0ull;
@@ -396,8 +397,11 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
         if (pq < PP) posmap[pq] = live ? pos : -1;
         if (l == 0) misc[0] = __builtin_popcountll(m);
     } else {
-        if (w == 1) {  // the zero row of PG and s0[PP]
-            for (int i = l; i < L; i += kWave) PG[PP * L + i] = T(0);
+        if (w == 1) {  // the zero rows of PG, PG2 and s0[PP]
+            for (int i = l; i < L; i += kWave) {
+                PG[PP * L + i] = T(0);
+                PG2[PP * L + i] = T(0);
+            }
             if (l == 0) s0[PP] = T(0);
         }
         const T* Wg = bf.W + (int64_t)r * n * ld;
@@ -558,7 +562,13 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
                 ckp = c;
             }
         };
+        // One barrier a round: p is double-buffered (PG, PG2) and so are the
+        // partial norms, and every lane re-derives "some row still moves" from
+        // the partials (a frozen row keeps |p|^2 <= 1, so live = |p|^2 > 1).
         for (int m = 0; m < kRParMaxIter; ++m) {
+            T* Pc = (m & 1) ? PG2 : PG;   // p of this round
+            T* Pn = (m & 1) ? PG : PG2;   // p of the next
+            T* np = npart + (m & 1) * PP * NB;
             typename M::acc_t qs[kTasks];
             rmark(4);
 #pragma unroll
@@ -583,7 +593,7 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
                     for (int s8 = 0; s8 < 8; ++s8) {
                         const int k = kb + 4 * s8 + kq;
                         const bool ok = kb + 4 * s8 < NP;  // compile time
-                        av[s8] = ok ? PG[ar2 * L + k] : T(0);
+                        av[s8] = ok ? Pc[ar2 * L + k] : T(0);
                         if (i == 0 && NB <= 4) bv[s8] = ok ? kf[(kb / 4 + s8) % KS] : T(0);
                         else bv[s8] = ok ? K[k * L + bc] : T(0);
                     }
@@ -594,11 +604,6 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
                 qs[i] = acc;
             }
             rmark(0);
-            __syncthreads();  // P read by every task; the row blocks' live flags for round m complete
-            rmark(1);
-            const int* fl = misc + 2 + 3 * (m & 1);
-            if ((fl[0] | fl[1] | fl[2]) == 0) break;
-            ckr[3] += 1;
 #pragma unroll
             for (int i = 0; i < kTasks; ++i) {
                 const int task = w + i * nw;
@@ -608,37 +613,47 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
                 for (int q = 0; q < 4; ++q) {
                     const int vr = tm * 16 + M::row(l, q), row = orow[i][q];
                     ps[i][q] = lv[i][q] ? ps[i][q] - T(2) * lr * qs[i][q] - cs[i][q] * ps[i][q] : ps[i][q];
-                    PG[row * L + tn * 16 + (l & 15)] = ps[i][q];  // the zero row stays zero
+                    Pn[row * L + tn * 16 + (l & 15)] = ps[i][q];  // the zero rows stay zero
                     T v = ps[i][q] * ps[i][q];
                     v += dpp_ror<8>(v);
                     v += dpp_ror<4>(v);
                     v += dpp_ror<2>(v);
                     v += dpp_ror<1>(v);
-                    if ((l & 15) == 0) npart[vr * NB + tn] = v;
+                    if ((l & 15) == 0) np[vr * NB + tn] = v;
                 }
             }
             rmark(2);
-            __syncthreads();  // P and the partial norms of this round
+            __syncthreads();  // p and the partial norms of this round
             rmark(1);
+            ckr[3] += 1;
 #pragma unroll
             for (int i = 0; i < kTasks; ++i) {
                 const int task = w + i * nw;
                 if (task >= ntask) break;
-                const int tm = task / NB, tn = task % NB;
+                const int tm = task / NB;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int vr = tm * 16 + M::row(l, q);
                     T pp[kConsNB];
 #pragma unroll
-                    for (int c = 0; c < NB; ++c) pp[c] = npart[vr * NB + c];
+                    for (int c = 0; c < NB; ++c) pp[c] = np[vr * NB + c];
                     T nr = T(0);
 #pragma unroll
                     for (int c = 0; c < NB; ++c) nr += pp[c];
                     lv[i][q] = lv[i][q] && nr > T(1);
                 }
-                const uint64_t any = __ballot(lv[i][0] || lv[i][1] || lv[i][2] || lv[i][3]);
-                if (tn == 0 && l == 0) misc[2 + 3 * ((m + 1) & 1) + tm] = any != 0;
             }
+            bool more = false;  // lane v: violator row v (nviol <= PP <= kWave)
+            if (l < nviol) {
+                T pp[kConsNB];
+#pragma unroll
+                for (int c = 0; c < NB; ++c) pp[c] = np[l * NB + c];
+                T nr = T(0);
+#pragma unroll
+                for (int c = 0; c < NB; ++c) nr += pp[c];
+                more = nr > T(1);
+            }
+            if (!__ballot(more)) break;  // the same verdict in every wave
         }
         // G replaces P (every read of P is behind the last barrier): the
         // violators' slices, zeros on the other rows
