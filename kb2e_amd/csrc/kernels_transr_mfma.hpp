@@ -70,6 +70,35 @@ __device__ __forceinline__ void block_gemm(int MT, int NT, int K, FA A, FB B, FP
     }
 }
 
+// block_gemm over a K whose bound KP is a compile-time multiple of 16 (the NP
+// padding of an image): loads without runtime guards, MFMAs only below K4.
+template <typename T, int KP, class FA, class FB, class FP>
+__device__ __forceinline__ void block_gemm_k(int MT, int NT, int K4, FA A, FB B, FP put) {
+    using M = Mfma16<T>;
+    const int l = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int idx = w; idx < MT * NT; idx += nw) {
+        const int mb = idx / NT, nb = idx % NT;
+        typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
+        const int ar = mb * 16 + (l & 15), bc = nb * 16 + (l & 15), kq = l >> 4;
+#pragma unroll
+        for (int kb = 0; kb < KP; kb += 32) {
+            T av[8], bv[8];
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const int k = kb + 4 * s + kq;
+                const bool ok = kb + 4 * s < KP;  // compile time
+                av[s] = ok ? A(ar, k) : T(0);
+                bv[s] = ok ? B(k, bc) : T(0);
+            }
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (kb + 4 * s < K4) acc = M::mma(av[s], bv[s], acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) put(mb * 16 + M::row(l, r), bc, acc[r]);
+    }
+}
+
 __host__ __device__ constexpr int rm_np(int n) { return (n + 15) & ~15; }
 __host__ __device__ constexpr int rm_ld(int n) { return rm_np(n) + 2; }
 __host__ __device__ constexpr int rm_up16(int v) { return (v + 15) & ~15; }
@@ -145,14 +174,15 @@ __device__ __forceinline__ void matvec_t(const T* WT, int L, int n, const T* xl,
 
 // Tile: phase A (projections, energies / compat projections, x, d, y = W x) and
 // the gradient partials dW = D^T X, dr, as transr_tile_kernel.
-template <typename T, bool PROJ, bool GRAD>
+template <typename T, bool PROJ, bool GRAD, int kNB>
 __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParBufs<T> bf) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int t = a.tile_first[a.batch_seg[a.batch]] + blockIdx.x;
     if (t >= a.tile_first[a.batch_seg[a.batch + 1]]) return;
     int r, e0, cnt;
     tile_range(a, t, r, e0, cnt);
-    const int n = a.n, ld = a.ld, NP = rm_np(n), L = rm_ld(n);
+    constexpr int NP = 16 * kNB, L = NP + 2;  // kNB = rm_np(n) / 16, exactly
+    const int n = a.n, ld = a.ld;
     const int MV = rm_up16(4 * a.St), UY = rm_up16(2 * a.St);
     T* Wl = (T*)smem;
     T* V = Wl + (PROJ ? NP * L : 0);
@@ -188,7 +218,7 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
     }
     __syncthreads();
     if (PROJ) {
-        block_gemm<T>(MV / 16, NP / 16, rm_k4(n), [&](int m, int k) { return V[m * L + k]; },
+        block_gemm_k<T, NP>(MV / 16, kNB, rm_k4(n), [&](int m, int k) { return V[m * L + k]; },
                       [&](int k, int c) { return Wl[k * L + c]; }, [&](int m, int c, T v) { P[m * L + c] = v; });
         __syncthreads();
         // one wave per sample: energies, hinge, x, d (transr/trainer.cpp:147-164, transr/transr.cpp:26-35)
@@ -258,7 +288,7 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
         }
         __syncthreads();
         // y = W x for every update (transr/trainer.cpp:168-169): Y = X W^T
-        block_gemm<T>(UY / 16, NP / 16, rm_k4(n), [&](int m, int k) { return X[m * L + k]; },
+        block_gemm_k<T, NP>(UY / 16, kNB, rm_k4(n), [&](int m, int k) { return X[m * L + k]; },
                       [&](int k, int c) { return Wl[c * L + k]; }, [&](int m, int c, T v) {
                           if (m < 2 * cnt && c < n) bf.y[((int64_t)kks[m >> 1] * 2 + (m & 1)) * ld + c] = v;
                       });
@@ -285,7 +315,7 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
     __syncthreads();
     // dW[j][i] = sum_u D[u][j] X[u][i]  (transr/trainer.cpp:166-167), this tile's partial
     T* wp = bf.wpart + (int64_t)blockIdx.x * n * ld;
-    block_gemm<T>(NP / 16, NP / 16, UY, [&](int j, int u) { return D[u * L + j]; },
+    block_gemm<T>(kNB, kNB, UY, [&](int j, int u) { return D[u * L + j]; },
                   [&](int u, int i) { return X[u * L + i]; }, [&](int j, int i, T v) {
                       if (j < n && i < n) wp[(int64_t)j * ld + i] = v;
                   });
