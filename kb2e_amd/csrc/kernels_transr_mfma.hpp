@@ -525,7 +525,7 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
     __syncthreads();
     if (misc[1] != 0) {
         // K = W0^T W0 (symmetric, zero past n) and s0 = a0.a0
-        block_gemm<T>(NB, NB, rm_k4(n), [&](int m, int k) { return Wl[k * L + m]; },
+        block_gemm_k<T, NP>(NB, NB, rm_k4(n), [&](int m, int k) { return Wl[k * L + m]; },
                       [&](int k, int c) { return Wl[k * L + c]; }, [&](int m, int c, T v) { K[m * L + c] = v; });
         for (int row = w; row < nrows; row += nw) {
             T ss = T(0);
@@ -735,7 +735,7 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
         return;
     }
     // pair records da = -lr W0 G (B(k, c) = W0[c][k])
-    block_gemm<T>(MR / 16, NB, rm_k4(n), [&](int m, int k) { return PG[m * L + k]; },
+    block_gemm_k<T, NP>(MR / 16, NB, rm_k4(n), [&](int m, int k) { return PG[m * L + k]; },
                   [&](int k, int c) { return Wl[c * L + k]; }, [&](int m, int c, T v) {
                       if (m >= nrows || c >= n || !vio[m]) return;
                       const int sl = slot_of[rowmap[m]];
