@@ -123,9 +123,11 @@ __host__ __device__ constexpr size_t rmfma_cons_lds(int n, int St) {
            sizeof(int) * (6 * (size_t)rm_up16(4 * St + 1) + 8);
 }
 
-template <typename T>
+// NP: the padded width rm_np(n), a compile-time constant at the call sites
+// (index arithmetic by constants, not runtime integer division)
+template <typename T, int NP>
 __device__ __forceinline__ void stage_matrix_padded(T* Wl, const T* Wg, int n, int ld) {
-    const int NP = rm_np(n), L = rm_ld(n);
+    constexpr int L = NP + 2;
 #pragma unroll 8
     for (int idx = threadIdx.x; idx < NP * L; idx += blockDim.x) {
         const int j = idx / L, i = idx % L;
@@ -135,9 +137,9 @@ __device__ __forceinline__ void stage_matrix_padded(T* Wl, const T* Wg, int n, i
 
 // rows[row][0..L) = table row ids[row] (zeros past n, or for ids < 0), every
 // thread of the block issuing independent loads (no per-row dependent chains).
-template <typename T>
+template <typename T, int NP>
 __device__ __forceinline__ void gather_rows(T* rows, const int* ids, int nrows, const T* table, int n, int ld) {
-    const int L = rm_ld(n);
+    constexpr int L = NP + 2;
 #pragma unroll 8
     for (int idx = threadIdx.x; idx < nrows * L; idx += blockDim.x) {
         const int row = idx / L, i = idx % L;
@@ -206,7 +208,7 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
         }
         ids[row] = e;
     }
-    if (PROJ) stage_matrix_padded(Wl, bf.W + (int64_t)r * n * ld, n, ld);
+    if (PROJ) stage_matrix_padded<T, NP>(Wl, bf.W + (int64_t)r * n * ld, n, ld);
     for (int idx = threadIdx.x; idx < UY * L; idx += blockDim.x) {
         X[idx] = T(0);
         if (GRAD) D[idx] = T(0);
@@ -214,7 +216,7 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
     for (int idx = threadIdx.x; idx < UY; idx += blockDim.x) coef[idx] = T(0);
     __syncthreads();
     if (PROJ) {  // V rows 4q + {0,1,2,3} = h, t, h', t' of sample q (zeros past the data)
-        gather_rows(V, ids, MV, bf.ent, n, ld);
+        gather_rows<T, NP>(V, ids, MV, bf.ent, n, ld);
     }
     __syncthreads();
     if (PROJ) {
