@@ -3,11 +3,21 @@
 
 A "step" is one batch of Trainer::bfgs (common/trainer.cpp:75-100): floor(|train|
 / batches) samples, each = 1 training triple + 1 Bernoulli-corrupted triple,
-scored, hinge-tested and applied with the reference's ordered norm updates.
-Workload = BASELINE.json configs[1]: TransE n=100 bern on FB15k (synthetic
-FB15k-shaped data, 14,951 entities / 1,345 relations / 483,142 triples), FP64
+scored, hinge-tested and applied.  Workload (default) = BASELINE.json's north-star
+target, configs[3]: TransR n=50 bern L1 on FB15k (synthetic FB15k-shaped data,
+14,951 entities / 1,345 relations / 483,142 triples), TransE-init: the seed
+tables come from a TransE n=50 unif run (ORDERED schedule = the reference's
+exact semantics) written and read back as the reference's `%.6lf` seed files
+(transr/trainer.cpp:88-113); the CPU baseline reads the very same files.  FP64
 like the reference.  `value` = training triples (samples) per second over the
-whole job, inputs resident in HBM; epochs' sampling + index build included.
+whole job, inputs resident in HBM.
+
+Timing: warmup runs W batches and then on to the next epoch boundary, so the
+K timed batches always start an epoch: the epoch's sampling commit, its event
+index (keys, radix sort, segments) and the prefetch of the next epoch's sample
+stream are inside the timed region (for K < batches this over-weights the
+per-epoch work; `epoch` in each schedule's record is one whole epoch timed the
+same way).
 
 Schedules (include/kb2e_engine.h kb2e_schedule): `value` is the PARALLEL
 schedule (the data-parallel form: the reference's sample stream, snapshot
@@ -49,6 +59,45 @@ CONFIGS = {
     "transr_k5": ("R", "k5", 100, 1, 0, 0.001),
 }
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+SEED_EPOCHS = 100  # TransE epochs behind the TransR seed tables ("TransE-init")
+
+
+def host_cpu():
+    """lscpu model name and the host's CPU count."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(),
+            "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
+
+
+def transe_seed(ds, dim, seed_dir, epochs=SEED_EPOCHS, device=0):
+    """TransR's TransE-init (transr/trainer.cpp:88-113): TransE n=dim, unif, on the
+    GPU with the ORDERED schedule (the reference's exact semantics), written as the
+    reference writes it (entity2vec.unif / relation2vec.unif, "%.6lf\t",
+    common/trainer.cpp:109-127) and read back, so GPU and CPU runs start from
+    the same quantised tables."""
+    from kb2e_amd.engine import Engine
+
+    eng = Engine("E", dim, ds.num_entities, ds.num_relations, rate=0.001, method=0, seed=7, device=device,
+                 schedule="ordered")
+    eng.upload_triples(ds.train)
+    eng.init_params()
+    for _ in range(epochs):
+        eng.train_batches(100)
+    eng.synchronize()
+    ent, rel, _ = eng.download_params()
+    eng.close()
+    os.makedirs(seed_dir, exist_ok=True)
+    data.write_table(os.path.join(seed_dir, "entity2vec.unif"), ent)
+    data.write_table(os.path.join(seed_dir, "relation2vec.unif"), rel)
+    return (data.read_table(os.path.join(seed_dir, "entity2vec.unif"), ds.num_entities, dim),
+            data.read_table(os.path.join(seed_dir, "relation2vec.unif"), ds.num_relations, dim))
 
 
 def algorithmic_bytes_per_sample(model, n, s, active_frac):
@@ -81,7 +130,7 @@ def _ref_epoch_seconds(cmd, e1, e2, limit_s):
     return (wall[1] - wall[0]) / (e2 - e1)
 
 
-def cpu_baseline(cfg_name, ds, budget_s=25.0):
+def cpu_baseline(cfg_name, ds, seed_dir=None, budget_s=25.0):
     """The reference itself (oracle/_ref, compiled from the reference sources)
     on this host, single-threaded, on the same synthetic dataset; falls back to
     the C restatement (oracle/liborc.so) when the binary is absent."""
@@ -97,18 +146,11 @@ def cpu_baseline(cfg_name, ds, budget_s=25.0):
                    "--distance", str(distance), "--rate", str(rate), "--seed", "7"]
             seed_note = ""
             if model == "R":
-                # TransR starts from TransE embeddings (transr/trainer.cpp:88-113): one
-                # reference TransE epoch, unif, writes the seed files
-                seed = os.path.join(d, "seed")
-                os.mkdir(seed)
-                subprocess.run([os.path.join(ROOT, "oracle", "_ref", "trainTransE"), "--datadir", d, "--outdir",
-                                seed, "--size", str(dim), "--method", "0", "--epochs", "1", "--seed", "7"],
-                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=budget_s * 4,
-                               check=True)
-                cmd += ["--seeddatadir", seed, "--seedmethod", "0"]
-                seed_note = ", seeded by one reference TransE epoch"
+                # the same TransE seed files the GPU run read (transr/trainer.cpp:88-113)
+                cmd += ["--seeddatadir", seed_dir, "--seedmethod", "0"]
+                seed_note = f", seeded from the GPU run's TransE-init files ({SEED_EPOCHS} TransE epochs)"
             per_epoch = _ref_epoch_seconds(cmd, e1, e2, budget_s * 4)
-        return {"value": S / per_epoch, "unit": "triples/s", "cores": 1, "kind": "reference",
+        return {"value": S / per_epoch, "unit": "triples/s", "cores": 1, "kind": "reference", **host_cpu(),
                 "sample": f"{os.path.basename(binary)} (compiled from the reference sources) on the same synthetic "
                           f"{shape}-shaped data{seed_note}, 1 thread pinned to one core; per-epoch time = (wall of "
                           f"{e2} epochs - wall of {e1}) / {e2 - e1}, {S} samples per epoch"}
@@ -119,8 +161,8 @@ def cpu_baseline(cfg_name, ds, budget_s=25.0):
     orc.srand(7)
     m.prep_train()
     if model == "R":
-        e, r, _ = m.tables()
-        m.transr_seed(e, r)
+        m.transr_seed(data.read_table(os.path.join(seed_dir, "entity2vec.unif"), ds.num_entities, dim),
+                      data.read_table(os.path.join(seed_dir, "relation2vec.unif"), ds.num_relations, dim))
     B = m.batch_size()
     t0 = time.time()
     nb = 0
@@ -128,7 +170,7 @@ def cpu_baseline(cfg_name, ds, budget_s=25.0):
         m.train_batches(1)
         nb += 1
     dt = time.time() - t0
-    return {"value": nb * B / dt, "unit": "triples/s", "cores": 1, "kind": "port",
+    return {"value": nb * B / dt, "unit": "triples/s", "cores": 1, "kind": "port", **host_cpu(),
             "sample": f"{nb} batches ({B} samples each) of the C restatement, 1 thread"}
 
 
@@ -138,7 +180,7 @@ def phase_bytes(model, n, s, a):
     return score_b, fold_b
 
 
-def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup):
+def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, seed_tabs=None):
     """Train `warmup` then time `steps` batches of one schedule; returns a dict."""
     from kb2e_amd.engine import Engine
 
@@ -159,9 +201,9 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup):
         w = np.broadcast_to(np.eye(dim), (ds.num_relations, dim, dim)).reshape(eng.wshape())  # identity Mr
         eng.upload_params(ent, rel, np.ascontiguousarray(w))
     else:
-        ent, rel, w = eng.init_params()
+        eng.init_params()  # consumes the reference's init draws (also for TransR, transr/trainer.cpp:70-86)
         if model == "R":
-            eng.transr_seed(ent, rel)  # seed = the init draws (no TransE run in the bench)
+            eng.transr_seed(*seed_tabs)
     B = len(train) // batches
     merger = None
     if world > 1:
@@ -179,20 +221,29 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup):
                 merger.merge()
     run.pos = 0
 
+    def to_epoch_start():
+        if run.pos % batches:
+            run(batches - run.pos % batches)
+
+    def timed(k):
+        eng.synchronize()
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        run(k)
+        eng.synchronize()
+        if dist is not None:
+            dist.barrier()
+        return time.perf_counter() - t0
+
     run(warmup)
+    to_epoch_start()  # the timed batches start an epoch (its sampling commit + index build inside)
     eng.synchronize()
     eng.take_stats()
     # HIP-event timing of the batch kernels on every 10th batch (events cost
-    # device time; sampling keeps the timed run unperturbed)
+    # device time; sampling keeps the timed run unperturbed); per-epoch kernels always
     eng.profile(10)
-    if dist is not None:
-        dist.barrier()
-    t0 = time.perf_counter()
-    run(steps)
-    eng.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(steps)
     loss, active = eng.take_stats()
     # phase B span: TransE/TransH "fold_phase" (ordered: per-row folds; parallel:
     # the apply kernels), TransR "apply" (parallel) or the relation owners (ordered)
@@ -205,10 +256,15 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup):
     fold_ms, fold_n = eng.profile_query(fold_name)
     score_ms, score_n = eng.profile_query("score")
     kernels_us = {}
-    for k in ("score", "fold", "fold_long", "apply", "tickets", "desc", "relowner", "fold_phase"):
+    for k in ("score", "fold", "fold_long", "apply", "tickets", "desc", "relowner", "fold_phase", "index", "sample"):
         ms, n = eng.profile_query(k)
         if n:
             kernels_us[k] = ms / n * 1e3
+    epoch_s = None
+    if not args.no_epoch:
+        eng.profile(0)
+        to_epoch_start()
+        epoch_s = timed(batches)
     eng.close()
     samples = steps * B
     if dist is not None:
@@ -239,8 +295,18 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup):
             traffic = float(v) if v else None
         except (OSError, ValueError):
             traffic = None
+    epoch_rec = None
+    if epoch_s is not None:
+        if dist is not None:
+            import torch
+
+            t = torch.tensor([epoch_s], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            epoch_s = float(t[0])
+        epoch_rec = {"value": batches * B * world / epoch_s, "ms": epoch_s * 1e3, "batches": batches}
     return {
         "value": samples / elapsed, "ms_per_step": elapsed / steps * 1e3, "B": B, "batches": batches,
+        "epoch": epoch_rec,
         "active_fraction": a,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": dominant,
@@ -252,14 +318,16 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--config", default="transe_fb15k", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="transr_fb15k", choices=sorted(CONFIGS))
     ap.add_argument("--precision", type=int, default=64, choices=[32, 64])
     ap.add_argument("--schedule", default="parallel", choices=["ordered", "parallel"],
                     help="schedule of the headline value; the other one is reported beside it")
     ap.add_argument("--only", action="store_true", help="measure the --schedule only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-epoch", action="store_true", help="skip the whole-epoch timing")
+    ap.add_argument("--seed-epochs", type=int, default=SEED_EPOCHS)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -279,11 +347,16 @@ def main():
     model, shape, dim, method, distance, rate = CONFIGS[args.config]
     ds = data.synthetic(shape, seed=1 if shape == "k5" else 0)
     train = shard_heads(ds.train, rank, world) if world > 1 else ds.train
-    main_run = measure(args, args.schedule, ds, train, rank, world, local, dist, args.steps, args.warmup)
+    seed_tmp = tempfile.TemporaryDirectory()
+    seed_tabs = None
+    if model == "R" and shape != "k5":
+        # every rank draws the same seed (fixed glibc seed), no broadcast needed
+        seed_tabs = transe_seed(ds, dim, seed_tmp.name, epochs=args.seed_epochs, device=local if world > 1 else 0)
+    main_run = measure(args, args.schedule, ds, train, rank, world, local, dist, args.steps, args.warmup, seed_tabs)
     other = "ordered" if args.schedule == "parallel" else "parallel"
     other_run = None
     if not args.only:
-        other_run = measure(args, other, ds, train, rank, world, local, dist, args.steps, args.warmup)
+        other_run = measure(args, other, ds, train, rank, world, local, dist, args.steps, args.warmup, seed_tabs)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -303,22 +376,28 @@ def main():
         "vs_baseline": None,
         "dtype": "f64" if args.precision == 64 else "f32",
         "data": f"synthetic {shape}-shaped (kb2e_amd.data.synthetic, seed {1 if shape == 'k5' else 0}), reference "
-                f"glibc sample stream seed 7" + (", numpy-drawn unit-row tables, identity Mr" if shape == "k5" else ""),
+                f"glibc sample stream seed 7" + (", numpy-drawn unit-row tables, identity Mr" if shape == "k5" else "")
+                + (f", TransE-init: {args.seed_epochs} TransE n={dim} unif epochs (ORDERED), %.6lf seed files"
+                   if seed_tabs is not None else ""),
         "config": {"workload": f"{args.config}: {'TransE' if model == 'E' else 'TransH' if model == 'H' else 'TransR'} "
                                f"n={dim} {'bern' if method else 'unif'} L{distance + 1}, {batches} batches of {B} "
-                               f"per GPU, {args.schedule} schedule",
+                               f"per GPU, {args.schedule} schedule"
+                               + (", compat energy, TransE-init" if model == "R" and shape != "k5" else ""),
                    "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "single",
                    "schedule": args.schedule},
         "roofline": main_run["roofline"],
         "active_fraction": main_run["active_fraction"],
+        "timing": "K batches from an epoch boundary (epoch sampling commit + index build inside)",
     }
+    out["schedules"] = {args.schedule: {"value": main_run["value"], "ms_per_step": main_run["ms_per_step"],
+                                        "epoch": main_run["epoch"]}}
     if other_run is not None:
-        out["schedules"] = {args.schedule: {"value": main_run["value"], "ms_per_step": main_run["ms_per_step"]},
-                            other: {"value": other_run["value"], "ms_per_step": other_run["ms_per_step"],
-                                    "roofline": other_run["roofline"]}}
+        out["schedules"][other] = {"value": other_run["value"], "ms_per_step": other_run["ms_per_step"],
+                                   "epoch": other_run["epoch"], "active_fraction": other_run["active_fraction"],
+                                   "roofline": other_run["roofline"]}
     if not args.no_cpu_baseline and world == 1:
         try:
-            out["cpu_baseline"] = cpu_baseline(args.config, ds)
+            out["cpu_baseline"] = cpu_baseline(args.config, ds, seed_tmp.name)
         except Exception as e:  # the baseline is reported, never the target
             out["cpu_baseline"] = {"value": None, "error": str(e)}
     print(json.dumps(out))

@@ -18,7 +18,7 @@ def test_bench_two_ranks_one_device(config):
     env = dict(os.environ, KB2E_DIST_ONE_DEVICE="1", KB2E_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", "29517" if config == "transe_fb15k" else "29518", os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "120", "--warmup", "10", "--config", config, "--only", "--no-cpu-baseline"]
+           "--gpus", "2", "--steps", "120", "--warmup", "10", "--config", config, "--only", "--no-cpu-baseline", "--no-epoch", "--seed-epochs", "3"]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]

@@ -113,7 +113,8 @@ def _transr_vs_model(ds, dim, epochs, monkeypatch, *, St=8, compat=False, distan
 
 
 @pytest.mark.parametrize("mfma", [True, False])
-@pytest.mark.parametrize("dim,distance,St", [(20, 0, 8), (20, 1, 4), (50, 0, 8), (33, 0, 2), (40, 0, 8), (64, 0, 1)])
+@pytest.mark.parametrize("dim,distance,St", [(20, 0, 8), (20, 1, 4), (50, 0, 8), (33, 0, 2), (40, 0, 8), (64, 0, 1),
+                                             (65, 0, 2), (96, 0, 8), (100, 0, 8), (100, 1, 4), (128, 0, 1)])
 def test_transr_parallel_fixed(dim, distance, St, mfma, monkeypatch):
     """Fixed (zeroed) energy; tiles of St samples (several per hot relation); the
     matrix-core kernels and the VALU ones.  St must not exceed the engine's own
@@ -122,9 +123,12 @@ def test_transr_parallel_fixed(dim, distance, St, mfma, monkeypatch):
 
 
 @pytest.mark.parametrize("mfma", [True, False])
-def test_transr_parallel_compat(mfma, monkeypatch):
-    """The reference's accumulating work-vector energy (transr/transr.cpp:20-25)."""
-    _transr_vs_model(tiny(), 20, 2, monkeypatch, St=8, compat=True, mfma=mfma)
+@pytest.mark.parametrize("dim,St", [(20, 8), (65, 2), (100, 8)])
+def test_transr_parallel_compat(dim, St, mfma, monkeypatch):
+    """The reference's accumulating work-vector energy (transr/transr.cpp:20-25).
+    n = 65: matrix-core images at St = 2; n = 100 (K5): the VALU tile kernels
+    (the f64 matrix-core transRNorm image does not fit the LDS there)."""
+    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=True, mfma=mfma)
 
 
 def test_transr_parallel_fp32_close(monkeypatch):

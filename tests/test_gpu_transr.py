@@ -45,10 +45,14 @@ def test_golden_training_run_fp64(name):
     assert [eng.rng_next() for _ in range(after.size)] == after.tolist()
 
 
-@pytest.mark.parametrize("compat,dim", [(False, 32), (True, 20), (False, 50)])
-def test_oracle_parity_with_transrnorm(compat, dim):
-    ds = data.synthetic("small", seed=4)
-    kw = dict(rate=0.005, margin=1.0, method=1, batches=25)
+@pytest.mark.parametrize("compat,dim,shape", [(False, 32, "small"), (True, 20, "small"), (False, 50, "small"),
+                                               (False, 65, "tiny"), (True, 96, "tiny"), (False, 100, "tiny"),
+                                               (True, 100, "tiny"), (False, 128, "tiny")])
+def test_oracle_parity_with_transrnorm(compat, dim, shape):
+    """dim <= 64: Mr rows in registers (transr_owner_reg_kernel); above: the
+    LDS-resident generic owner (engine_relowner.inc), K5's n = 100 included."""
+    ds = data.synthetic(shape, seed=4)
+    kw = dict(rate=0.005 if shape == "small" else 0.01, margin=1.0, method=1, batches=25 if shape == "small" else 10)
     m = oracle_model("R", ds, dim, transr_compat=compat, **kw)
     orc.srand(8)
     m.prep_train()
