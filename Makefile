@@ -32,11 +32,27 @@ kb2e_amd/libkb2e_prof.so: $(CSRC)
 oracle:
 	$(MAKE) -C oracle all
 
+# The reference-side binding (integration/gpu_trainer.h) compiled against the
+# reference's headers and objects (oracle/_ref/common.a, built from
+# /root/reference by `make ref`) and libkb2e.so.  Needs /root/reference; the
+# binaries travel to the GPU box in bin/binding/.
+REF ?= /root/reference
+BINDING := bin/binding/trainTransE bin/binding/trainTransH bin/binding/trainTransR
+
+binding: $(BINDING)
+
+bin/binding/train%: integration/train_gpu.cpp integration/gpu_trainer.h include/kb2e_engine.h kb2e_amd/libkb2e.so ref
+	@mkdir -p bin/binding
+	g++ -O2 -std=c++11 -Wall -I$(REF) -Iinclude -Iintegration \
+	    -DKB2E_BINDING_MODEL=$(if $(filter TransE,$*),0,$(if $(filter TransH,$*),1,2)) \
+	    -o $@ integration/train_gpu.cpp oracle/_ref/common.a -Lkb2e_amd -lkb2e \
+	    -Wl,-rpath,'$$ORIGIN/../../kb2e_amd'
+
 ref:
 	$(MAKE) -C oracle ref
 
 clean:
-	rm -f kb2e_amd/libkb2e.so bin/kb2e $(BINS)
+	rm -f kb2e_amd/libkb2e.so bin/kb2e $(BINS) $(BINDING)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle ref clean prof
+.PHONY: all oracle ref clean prof binding

@@ -1062,7 +1062,7 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
         return KB2E_EINVAL;
     if (g.model == KB2E_TRANSR && g.num_relations > g.num_entities) return KB2E_EINVAL;
     if (g.schedule == KB2E_SCHEDULE_PARALLEL && g.model == KB2E_TRANSR && g.dim > 128) return KB2E_EUNSUPPORTED;  // entityVec_next_[relation]
-    if (g.model == KB2E_TRANSR && ((size_t)g.dim * (g.dim + 1) + 3 * (size_t)g.dim) * (g.precision / 8) > 96 * 1024)
+    if (g.model == KB2E_TRANSR && ((size_t)g.dim * (g.dim + 1) + 3 * (size_t)g.dim) * (g.precision / 8) > 152 * 1024)
         return KB2E_EUNSUPPORTED;  // the owner's relation matrix must fit in LDS
     std::unique_ptr<kb2e_ctx> c(new kb2e_ctx());
     c->cfg = g;
