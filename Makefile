@@ -6,7 +6,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -Wall -Iinclude
 
-CSRC := $(wildcard kb2e_amd/csrc/*.hip kb2e_amd/csrc/*.hpp kb2e_amd/csrc/*.inc) include/kb2e_engine.h
+CSRC := $(filter-out kb2e_amd/csrc/eval.hip,$(wildcard kb2e_amd/csrc/*.hip kb2e_amd/csrc/*.hpp kb2e_amd/csrc/*.inc)) include/kb2e_engine.h
 
 BINS := bin/trainTransE bin/trainTransH bin/trainTransR bin/evalTransE bin/evalTransH bin/evalTransR
 
@@ -20,14 +20,24 @@ bin/kb2e: kb2e_amd/csrc/host/kb2e_cli.cpp include/kb2e_engine.h kb2e_amd/libkb2e
 $(BINS): bin/kb2e
 	ln -sf kb2e $@
 
-kb2e_amd/libkb2e.so: $(CSRC)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ kb2e_amd/csrc/engine.hip
+# two translation units (the training engine, the evaluator), compiled in parallel
+kb2e_amd/build/engine.o: $(CSRC)
+	@mkdir -p kb2e_amd/build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ kb2e_amd/csrc/engine.hip
+
+kb2e_amd/build/eval.o: kb2e_amd/csrc/eval.hip kb2e_amd/csrc/eval.hpp kb2e_amd/csrc/hip_util.hpp \
+		kb2e_amd/csrc/host_data.hpp kb2e_amd/csrc/kernels_common.hpp kb2e_amd/csrc/kernels_sampler.hpp
+	@mkdir -p kb2e_amd/build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ kb2e_amd/csrc/eval.hip
+
+kb2e_amd/libkb2e.so: kb2e_amd/build/engine.o kb2e_amd/build/eval.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 # diagnostic build: per-phase cycle counters in the relation-owner kernels
 prof: kb2e_amd/libkb2e_prof.so
 
-kb2e_amd/libkb2e_prof.so: $(CSRC)
-	$(HIPCC) $(HIPFLAGS) -DKB2E_OWNER_PROF -shared -o $@ kb2e_amd/csrc/engine.hip
+kb2e_amd/libkb2e_prof.so: $(CSRC) kb2e_amd/build/eval.o
+	$(HIPCC) $(HIPFLAGS) -DKB2E_OWNER_PROF -shared -o $@ kb2e_amd/csrc/engine.hip kb2e_amd/build/eval.o
 
 oracle:
 	$(MAKE) -C oracle all
@@ -52,7 +62,7 @@ ref:
 	$(MAKE) -C oracle ref
 
 clean:
-	rm -f kb2e_amd/libkb2e.so bin/kb2e $(BINS) $(BINDING)
+	rm -f kb2e_amd/libkb2e.so kb2e_amd/build/*.o bin/kb2e $(BINS) $(BINDING)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle ref clean prof binding

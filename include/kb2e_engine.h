@@ -153,10 +153,30 @@ kb2e_status kb2e_take_stats(kb2e_ctx* ctx, double* loss, int64_t* active);
  * raw hits@10, filtered mean rank, filtered hits@10 (hits as fractions, as
  * printed at :249-250).  Energies are bit-identical FP64 restatements of the
  * reference's; ties with the true triple are not counted above it.  TransR
- * uses the zeroed (fixed) work vectors.  Requires dim <= 128. */
+ * uses the zeroed (fixed) work vectors here; kb2e_evaluate_transr_compat is
+ * the reference evalTransR's stateful energy.  dim <= 600. */
 kb2e_status kb2e_evaluate(kb2e_ctx* ctx, const int32_t* heads, const int32_t* tails, const int32_t* relations,
                           int64_t ntest, const int32_t* filter_heads, const int32_t* filter_tails,
                           const int32_t* filter_relations, int64_t nfilter, double* out);
+
+/* TransR as the reference's evalTransR computes it: the energy work vectors
+ * are never zeroed (transr/transr.cpp:20-25, transr/evaluation.cpp:22-32), so
+ * every energy depends on all energies computed before it in the evaluator's
+ * cached relation-major loop (common/evaluation.cpp:107-121, 181-238; the
+ * per-relation energy cache is used when |E| <= 40000, common/evaluation.h:11).
+ * That sequence is replayed exactly in FP64 on the device.  `work` = 2 x dim
+ * doubles (head then tail work vector): in, the state to start from (NULL =
+ * zeros, as a fresh evalTransR process); out, the state after the run.
+ * out[0..3] as kb2e_evaluate; out[4] = candidates whose energy equals the true
+ * triple's (std::sort orders those arbitrarily, :138; they are ranked after
+ * the truth here).  `progress` (may be NULL) is called after each relation
+ * with the fraction of test triples done (the reference prints it, :240).
+ * dim <= 140. */
+kb2e_status kb2e_evaluate_transr_compat(kb2e_ctx* ctx, const int32_t* heads, const int32_t* tails,
+                                        const int32_t* relations, int64_t ntest, const int32_t* filter_heads,
+                                        const int32_t* filter_tails, const int32_t* filter_relations,
+                                        int64_t nfilter, double* work, double* out,
+                                        void (*progress)(double fraction, void* user), void* user);
 
 /* Raw glibc stream access (the context's RNG, as std::rand() in the reference). */
 int32_t kb2e_rng_next(kb2e_ctx* ctx);

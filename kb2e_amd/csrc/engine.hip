@@ -26,6 +26,8 @@
 
 #include "../../include/kb2e_engine.h"
 #include "glibc_rand.hpp"
+#include "hip_util.hpp"
+#include "eval.hpp"
 #include "host_data.hpp"
 #include "kernels_common.hpp"
 #include "kernels_index.hpp"
@@ -33,7 +35,6 @@
 #include "kernels_transe_long.hpp"
 #include "kernels_relowner.hpp"
 #include "kernels_sampler.hpp"
-#include "kernels_eval.hpp"
 #include "kernels_parallel.hpp"
 #include "kernels_transr_parallel.hpp"
 #include "kernels_transr_mfma.hpp"
@@ -43,18 +44,6 @@ using namespace kb2e;
 
 namespace {
 
-struct HipError : std::runtime_error {
-    using std::runtime_error::runtime_error;
-};
-
-#define HIPCHK(expr)                                                                              \
-    do {                                                                                          \
-        hipError_t _e = (expr);                                                                   \
-        if (_e != hipSuccess)                                                                     \
-            throw HipError(std::string(#expr) + ": " + hipGetErrorString(_e) + " @" +             \
-                           std::to_string(__LINE__));                                             \
-    } while (0)
-
 constexpr int kGlibcBlock = 4096;  // words per block of the device glibc generator
 
 int bits_for(int64_t v) {  // bits to hold values 0..v
@@ -62,25 +51,6 @@ int bits_for(int64_t v) {  // bits to hold values 0..v
     while ((1ll << b) <= v) ++b;
     return b;
 }
-
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    void alloc(size_t b) {
-        free();
-        if (b == 0) b = 16;
-        HIPCHK(hipMalloc(&p, b));
-        bytes = b;
-    }
-    void free() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-    template <class T>
-    T* as() const { return (T*)p; }
-    ~DevBuf() { free(); }
-};
 
 struct Timer {
     double ms = 0;
@@ -1378,113 +1348,51 @@ kb2e_status kb2e_train_epoch(kb2e_ctx* c, double* loss, int64_t* active) {
     });
 }
 
+namespace {
+EvalTables eval_tables(kb2e_ctx* c) {
+    EvalTables t{};
+    t.model = c->cfg.model;
+    t.n = c->n;
+    t.ld = c->ld;
+    t.ne = c->cfg.num_entities;
+    t.nr = c->cfg.num_relations;
+    t.l1 = c->cfg.distance == 0 || c->cfg.model == KB2E_TRANSH;
+    t.f64 = c->f64();
+    t.ent = c->ent.p;
+    t.rel = c->rel.p;
+    // ORDERED TransR keeps the committed matrices in wsnap (W_A)
+    t.w = c->cfg.model == KB2E_TRANSR && !c->parallel() ? c->wsnap.p : c->w.p;
+    t.stream = c->stream;
+    return t;
+}
+}  // namespace
+
 kb2e_status kb2e_evaluate(kb2e_ctx* c, const int32_t* th, const int32_t* tt, const int32_t* tr, int64_t ntest,
                           const int32_t* fh, const int32_t* ft, const int32_t* fr, int64_t nfilter, double* out) {
     return guarded(c, [&] {
-        if (!th || !tt || !tr || ntest < 1 || !out) return fail(c, KB2E_EINVAL, "empty test set");
-        if (c->n > 128) return fail(c, KB2E_EUNSUPPORTED, "evaluation supports dim <= 128");
+        if (!th || !tt || !tr || ntest < 1 || !out || (nfilter > 0 && (!fh || !ft || !fr)))
+            return fail(c, KB2E_EINVAL, "empty test set");
         if (!c->have_params) return fail(c, KB2E_ESTATE, "no embeddings on the device");
         HIPCHK(hipSetDevice(c->cfg.device));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        const int ne = c->cfg.num_entities, nr = c->cfg.num_relations, n = c->n;
-        // filter set (test + train + valid in the caller's order; duplicates are fine)
-        std::vector<int32_t> H(fh, fh + nfilter), T(ft, ft + nfilter), R(fr, fr + nfilter);
-        for (int64_t k = 0; k < nfilter; ++k)
-            if (H[k] < 0 || H[k] >= ne || T[k] < 0 || T[k] >= ne || R[k] < 0 || R[k] >= nr)
-                return fail(c, KB2E_EINVAL, "filter triple out of range");
-        FilterSet fs;
-        fs.build(H, T, R, ne, nr);
-        // test triples grouped by relation (the reference visits relations in id order)
-        std::vector<std::vector<int64_t>> byrel(nr);
-        for (int64_t k = 0; k < ntest; ++k) {
-            if (th[k] < 0 || th[k] >= ne || tt[k] < 0 || tt[k] >= ne || tr[k] < 0 || tr[k] >= nr)
-                return fail(c, KB2E_EINVAL, "test triple out of range");
-            byrel[tr[k]].push_back(k);
-        }
-        std::vector<int32_t> qh, qt;
-        std::vector<int64_t> qoff(nr + 1, 0);
-        for (int r = 0; r < nr; ++r) {
-            for (int64_t k : byrel[r]) {
-                qh.push_back(th[k]);
-                qt.push_back(tt[k]);
-            }
-            qoff[r + 1] = (int64_t)qh.size();
-        }
-        DevBuf d_slots, d_qh, d_qt, d_counts, d_target, d_PT, d_relv;
-        d_slots.alloc(fs.slots.size() * 8);
-        HIPCHK(hipMemcpy(d_slots.p, fs.slots.data(), fs.slots.size() * 8, hipMemcpyHostToDevice));
-        d_qh.alloc(qh.size() * 4);
-        d_qt.alloc(qt.size() * 4);
-        HIPCHK(hipMemcpy(d_qh.p, qh.data(), qh.size() * 4, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(d_qt.p, qt.data(), qt.size() * 4, hipMemcpyHostToDevice));
-        d_counts.alloc(qh.size() * 4 * 8);
-        HIPCHK(hipMemset(d_counts.p, 0, d_counts.bytes));
-        d_target.alloc(qh.size() * 2 * 8);
-        d_PT.alloc((size_t)n * ne * 8);
-        d_relv.alloc((size_t)n * 8);
-        HIPCHK(hipDeviceSynchronize());  // legacy-stream memset/copies above vs the engine stream
-        for (int r = 0; r < nr; ++r) {
-            const int64_t nq = qoff[r + 1] - qoff[r];
-            if (nq == 0) continue;
-            c->timed("eval", [&] {
-                const int pg = (std::max(ne, n) + 255) / 256;
-                if (c->f64()) {
-                    EvalArgs<double> ea{c->cfg.model, n, c->ld, ne, c->cfg.distance == 0 || c->cfg.model == KB2E_TRANSH,
-                                        c->ent.as<double>(), c->rel.as<double>(),
-                                        c->cfg.model == KB2E_TRANSR && !c->parallel() ? c->wsnap.as<double>() : c->w.as<double>(), r,
-                                        d_PT.as<double>(), d_relv.as<double>()};
-                    eval_project_kernel<double><<<pg, 256, 0, c->stream>>>(ea);
-                } else {
-                    EvalArgs<float> ea{c->cfg.model, n, c->ld, ne, c->cfg.distance == 0 || c->cfg.model == KB2E_TRANSH,
-                                       c->ent.as<float>(), c->rel.as<float>(),
-                                       c->cfg.model == KB2E_TRANSR && !c->parallel() ? c->wsnap.as<float>() : c->w.as<float>(), r,
-                                       d_PT.as<double>(), d_relv.as<double>()};
-                    eval_project_kernel<float><<<pg, 256, 0, c->stream>>>(ea);
-                }
-                HIPCHK(hipGetLastError());
-                RankArgs ra{};
-                ra.PT = d_PT.as<double>();
-                ra.relv = d_relv.as<double>();
-                ra.n = n;
-                ra.ne = ne;
-                ra.l1 = c->cfg.distance == 0 || c->cfg.model == KB2E_TRANSH;
-                ra.r = r;
-                ra.qh = d_qh.as<int32_t>() + qoff[r];
-                ra.qt = d_qt.as<int32_t>() + qoff[r];
-                ra.nq = (int32_t)nq;
-                ra.slots = d_slots.as<uint64_t>();
-                ra.mask = fs.mask;
-                ra.nr64 = (uint64_t)nr;
-                ra.ne64 = (uint64_t)ne;
-                ra.counts = d_counts.as<unsigned long long>() + qoff[r] * 4;
-                ra.target = d_target.as<double>() + qoff[r] * 2;
-                eval_target_kernel<<<(int)((nq + 255) / 256), 256, 0, c->stream>>>(ra);
-                HIPCHK(hipGetLastError());
-                dim3 grid((ne + 255) / 256, (unsigned)((nq + kQ - 1) / kQ));
-                eval_rank_kernel<<<grid, 256, 0, c->stream>>>(ra);
-                HIPCHK(hipGetLastError());
-            });
-        }
-        // the engine stream is non-blocking: wait for it before reading back
-        HIPCHK(hipStreamSynchronize(c->stream));
-        std::vector<unsigned long long> counts(qh.size() * 4);
-        HIPCHK(hipMemcpy(counts.data(), d_counts.p, counts.size() * 8, hipMemcpyDeviceToHost));
-        long long rawSum = 0, filtSum = 0, rawHits = 0, filtHits = 0;
-        for (size_t q = 0; q < qh.size(); ++q) {
-            for (int side = 0; side < 2; ++side) {
-                const long long raw = 1 + (long long)counts[q * 4 + 2 * side];
-                const long long filt = 1 + (long long)counts[q * 4 + 2 * side + 1];
-                rawSum += raw;
-                filtSum += filt;
-                rawHits += raw <= 10;
-                filtHits += filt <= 10;
-            }
-        }
-        const double nc = (double)ntest * 2.0;
-        out[0] = rawSum / nc;
-        out[1] = rawHits / nc;
-        out[2] = filtSum / nc;
-        out[3] = filtHits / nc;
+        c->timed("eval", [&] { evaluate_fixed(eval_tables(c), EvalQuery{th, tt, tr, ntest, fh, ft, fr, nfilter}, out); });
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_evaluate_transr_compat(kb2e_ctx* c, const int32_t* th, const int32_t* tt, const int32_t* tr,
+                                        int64_t ntest, const int32_t* fh, const int32_t* ft, const int32_t* fr,
+                                        int64_t nfilter, double* work, double* out,
+                                        void (*progress)(double fraction, void* user), void* user) {
+    return guarded(c, [&] {
+        if (!th || !tt || !tr || ntest < 1 || !out || (nfilter > 0 && (!fh || !ft || !fr)))
+            return fail(c, KB2E_EINVAL, "empty test set");
+        if (c->cfg.model != KB2E_TRANSR) return fail(c, KB2E_EUNSUPPORTED, "TransR only");
+        if (!c->have_params) return fail(c, KB2E_ESTATE, "no embeddings on the device");
+        HIPCHK(hipSetDevice(c->cfg.device));
+        c->timed("eval", [&] {
+            evaluate_transr_compat(eval_tables(c), EvalQuery{th, tt, tr, ntest, fh, ft, fr, nfilter}, work, out,
+                                   progress, user);
+        });
         return KB2E_OK;
     });
 }

@@ -1,0 +1,47 @@
+// hip_util.hpp -- host-side HIP helpers shared by the engine's translation
+// units (engine.hip, eval.hip): error checks that throw (turned into status
+// codes at the C ABI) and an owning device buffer.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+namespace kb2e {
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+#define HIPCHK(expr)                                                                              \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess)                                                                     \
+            throw ::kb2e::HipError(std::string(#expr) + ": " + hipGetErrorString(_e) + " @" +     \
+                                   std::string(__FILE__) + ":" + std::to_string(__LINE__));       \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    void alloc(size_t b) {
+        free();
+        if (b == 0) b = 16;
+        HIPCHK(hipMalloc(&p, b));
+        bytes = b;
+    }
+    void free() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const { return (T*)p; }
+    ~DevBuf() { free(); }
+};
+
+}  // namespace kb2e

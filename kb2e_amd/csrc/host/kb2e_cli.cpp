@@ -361,7 +361,8 @@ double vec_len(const double* a, int n) {
 }
 
 // EmbeddingEvaluation::prepare + run (common/evaluation.cpp:181-266) with the
-// ranking on the GPU (kb2e_evaluate).
+// ranking on the GPU (kb2e_evaluate; TransR with --transrcompat 1, the default:
+// kb2e_evaluate_transr_compat, the reference's stateful energy).
 int eval_main(int argc, char** argv, kb2e_model model) {
     EmbeddingArguments args = parseArgs(argc, argv);
     printf("%s\n", args.to_string().c_str());
@@ -411,9 +412,6 @@ int eval_main(int argc, char** argv, kb2e_model model) {
             exit(1);
         }
     }
-    if (model == KB2E_TRANSR && args.transrCompat)
-        fprintf(stderr, "note: TransR is ranked with zeroed energy work vectors (the reference's evaluator "
-                        "accumulates them across calls, transr/transr.cpp:20-25)\n");
     kb2e_config cfg;
     kb2e_default_config(&cfg);
     cfg.model = model;
@@ -427,10 +425,22 @@ int eval_main(int argc, char** argv, kb2e_model model) {
     kb2e_ctx* ctx = nullptr;
     check(nullptr, kb2e_create(&cfg, &ctx), "create");
     check(ctx, kb2e_upload_params(ctx, E.data(), R.data(), W.empty() ? nullptr : W.data()), "upload_params");
-    double out[4];
-    check(ctx, kb2e_evaluate(ctx, th.data(), tt.data(), tr.data(), (int64_t)th.size(), fh.data(), ft.data(),
-                             fr.data(), (int64_t)fh.size(), out), "evaluate");
-    printf("\rProcessed %05.2f%% ...", 100.0);
+    double out[5];
+    if (model == KB2E_TRANSR && args.transrCompat) {
+        // the reference's evalTransR: energy work vectors accumulate over the
+        // whole run (transr/transr.cpp:20-25); progress per relation (:240)
+        auto progress = [](double f, void*) {
+            printf("\rProcessed %05.2f%% ...", f * 100.0);
+            fflush(stdout);
+        };
+        check(ctx, kb2e_evaluate_transr_compat(ctx, th.data(), tt.data(), tr.data(), (int64_t)th.size(), fh.data(),
+                                               ft.data(), fr.data(), (int64_t)fh.size(), nullptr, out, progress,
+                                               nullptr), "evaluate");
+    } else {
+        check(ctx, kb2e_evaluate(ctx, th.data(), tt.data(), tr.data(), (int64_t)th.size(), fh.data(), ft.data(),
+                                 fr.data(), (int64_t)fh.size(), out), "evaluate");
+        printf("\rProcessed %05.2f%% ...", 100.0);
+    }
     printf("\n");
     printf("Raw      -- Rank: %f, Hits@10: %f\n", out[0], out[1]);
     printf("Filtered -- Rank: %f, Hits@10: %f\n", out[2], out[3]);

@@ -25,7 +25,7 @@ EXPORTS = [
     "kb2e_init_params", "kb2e_transr_seed", "kb2e_upload_params", "kb2e_download_params", "kb2e_get_transr_work",
     "kb2e_set_transr_work", "kb2e_set_sample_stream", "kb2e_get_sample_stream", "kb2e_train_epoch", "kb2e_train_batches",
     "kb2e_synchronize", "kb2e_take_stats", "kb2e_rng_next", "kb2e_profile_enable", "kb2e_profile_query",
-    "kb2e_device_bytes", "kb2e_device_tables", "kb2e_renormalize", "kb2e_evaluate",
+    "kb2e_device_bytes", "kb2e_device_tables", "kb2e_renormalize", "kb2e_evaluate", "kb2e_evaluate_transr_compat",
 ]
 
 
@@ -75,6 +75,8 @@ def lib():
                                          C.POINTER(i64), C.POINTER(i64)]),
             "kb2e_renormalize": (i32, [vp, u8p, u8p, u8p]),
             "kb2e_evaluate": (i32, [vp, i32p, i32p, i32p, i64, i32p, i32p, i32p, i64, dp]),
+            "kb2e_evaluate_transr_compat": (i32, [vp, i32p, i32p, i32p, i64, i32p, i32p, i32p, i64, dp, dp, vp,
+                                                  vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -237,6 +239,21 @@ class Engine:
         self._check(lib().kb2e_evaluate(self.h, _ip(tc[0]), _ip(tc[1]), _ip(tc[2]), len(test), _ip(fc[0]),
                                         _ip(fc[1]), _ip(fc[2]), len(filt), _dp(out)), "evaluate")
         return {"raw_rank": out[0], "raw_hits10": out[1], "filtered_rank": out[2], "filtered_hits10": out[3]}
+
+    def evaluate_transr_compat(self, test, filt, work=None):
+        """TransR link prediction with the reference evalTransR's accumulating
+        energy work vectors; returns the ranks plus "ties" and the final "work"."""
+        test = np.ascontiguousarray(test, dtype=np.int32)
+        filt = np.ascontiguousarray(filt, dtype=np.int32)
+        tc = [np.ascontiguousarray(test[:, k]) for k in range(3)]
+        fc = [np.ascontiguousarray(filt[:, k]) for k in range(3)]
+        w = np.zeros(2 * self.n) if work is None else np.ascontiguousarray(work, dtype=np.float64).reshape(-1).copy()
+        out = np.zeros(5)
+        self._check(lib().kb2e_evaluate_transr_compat(self.h, _ip(tc[0]), _ip(tc[1]), _ip(tc[2]), len(test),
+                                                      _ip(fc[0]), _ip(fc[1]), _ip(fc[2]), len(filt), _dp(w),
+                                                      _dp(out), None, None), "evaluate_transr_compat")
+        return {"raw_rank": out[0], "raw_hits10": out[1], "filtered_rank": out[2], "filtered_hits10": out[3],
+                "ties": int(out[4]), "work": w.reshape(2, self.n)}
 
     def device_bytes(self):
         return lib().kb2e_device_bytes(self.h)

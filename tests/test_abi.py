@@ -2,6 +2,8 @@
 every symbol include/kb2e_engine.h declares (no compute calls, no GPU)."""
 import ctypes
 import os
+
+import pytest
 import re
 import subprocess
 
@@ -41,9 +43,8 @@ def test_default_config_is_reference_defaults():
 
 
 def test_create_without_gpu_fails_loudly():
-    import torch
-    if torch.cuda.is_available():
-        return
+    if os.path.exists("/dev/kfd"):  # a GPU box: nothing to check
+        pytest.skip("GPU present")
     try:
         engine.Engine("E", 20, 10, 2, batches=1)
     except engine.EngineError:

@@ -102,3 +102,36 @@ def test_train_cli_parallel_schedule(tmp_path, prog, name):
         a = np.array(open(out / f).read().split(), dtype=np.float64)
         b = np.array(open(os.path.join(GOLDEN, name, f)).read().split(), dtype=np.float64)
         assert a.shape == b.shape and np.isfinite(a).all()
+
+
+def test_eval_transr_cli_compat(tmp_path):
+    """bin/evalTransR on the reference's transr_compat output files: the stateful
+    compat energy (the reference evalTransR's), printed as the reference prints
+    it; equal to the reference's lines up to the exact ties of that run."""
+    from gpu_common import tiny
+    from kb2e_amd import data
+    from kb2e_amd.engine import Engine
+
+    run = MANIFEST["runs"]["transr_compat"]
+    f = run["flags"]
+    d = os.path.join(GOLDEN, "transr_compat")
+    exe = tmp_path / "evalTransR"
+    exe.symlink_to(os.path.join(ROOT, "bin", "kb2e"))
+    res = subprocess.run([str(exe), "--datadir", os.path.join(GOLDEN, "tiny"), "--outdir", d, "--size",
+                          str(f["size"]), "--method", str(f["method"]), "--distance", str(f["distance"])],
+                         capture_output=True, text=True, timeout=300, check=True)
+    lines = {l.split("--")[0].strip().split("\r")[-1]: l for l in res.stdout.splitlines() if "Hits@10" in l}
+    got = {k: [float(x.split(":")[1]) for x in v.split("--")[1].split(",")] for k, v in lines.items()}
+    ds = tiny()
+    n = f["size"]
+    eng = Engine("R", n, ds.num_entities, ds.num_relations)
+    eng.upload_params(data.read_table(os.path.join(d, "entity2vec.bern"), ds.num_entities, n),
+                      data.read_table(os.path.join(d, "relation2vec.bern"), ds.num_relations, n),
+                      data.read_table(os.path.join(d, "weights.bern"), ds.num_relations * n, n).reshape(-1, n, n))
+    mine = eng.evaluate_transr_compat(ds.test, np.concatenate([ds.test, ds.train, ds.valid]))
+    assert got["Raw"] == pytest.approx([mine["raw_rank"], mine["raw_hits10"]], abs=5e-7)
+    assert got["Filtered"] == pytest.approx([mine["filtered_rank"], mine["filtered_hits10"]], abs=5e-7)
+    ev, n2 = run["eval"], 2 * len(ds.test)
+    assert abs(got["Filtered"][0] - ev["filtered"]["rank"]) * n2 <= mine["ties"] + 1e-3
+    assert abs(got["Raw"][0] - ev["raw"]["rank"]) * n2 <= mine["ties"] + 1e-3
+    assert "Processed 100.00%" in res.stdout

@@ -82,3 +82,102 @@ def test_eval_larger_set_matches_oracle(model, dim):
     assert exp["ties"] == 0
     for k in ("raw_rank", "raw_hits10", "filtered_rank", "filtered_hits10"):
         assert res[k] == pytest.approx(exp[k], abs=1e-12), k
+
+
+# ---------------------------------------------------------------- TransR compat
+# The reference's evalTransR never zeroes its energy work vectors
+# (transr/transr.cpp:20-25, transr/evaluation.cpp:22-32): every energy depends on
+# all energies computed before it in the cached relation-major loop
+# (common/evaluation.cpp:107-121, 181-238).  The device replays that chain in
+# the reference's operation order, so its energies are the oracle's bit for
+# bit: ranks, hits, tie counts and the final work vectors must be EQUAL.
+
+
+def _compat_vs_oracle(ds, n, ent, rel, w, *, distance=0, work=None, test=None):
+    test = ds.test if test is None else test
+    filt = np.concatenate([ds.test, ds.train, ds.valid])
+    eng = Engine("R", n, ds.num_entities, ds.num_relations, distance=distance)
+    eng.upload_params(ent, rel, w)
+    res = eng.evaluate_transr_compat(test, filt, work)
+    m = orc.Model("R", n, ds.num_entities, ds.num_relations, distance=distance, transr_compat=True)
+    m.set_tables(ent, rel, w)
+    w0 = np.zeros((2, n)) if work is None else np.asarray(work).reshape(2, n)
+    m.set_transr_work(w0[0], w0[1])
+    exp = m.evaluate(test, filt)
+    for k in ("raw_rank", "raw_hits10", "filtered_rank", "filtered_hits10", "ties"):
+        assert res[k] == exp[k], (k, res[k], exp[k])
+    hw, tw = m.transr_work()
+    assert np.array_equal(res["work"][0], hw) and np.array_equal(res["work"][1], tw)
+    return res
+
+
+def test_eval_transr_compat_matches_reference_binary():
+    """Golden: the reference evalTransR's printed numbers on the transr_compat run
+    (the oracle, and so the device, agree with them up to the exact ties)."""
+    run, ds, ent, rel, w = _load_run("transr_compat")
+    res = _compat_vs_oracle(ds, run["flags"]["size"], ent, rel, w)
+    ev, n2 = run["eval"], 2 * len(ds.test)
+    assert res["ties"] > 0
+    assert abs(res["filtered_rank"] - ev["filtered"]["rank"]) * n2 <= res["ties"] + 1e-6
+    assert abs(res["raw_rank"] - ev["raw"]["rank"]) * n2 <= res["ties"] + 1e-6
+    assert abs(res["filtered_hits10"] - ev["filtered"]["hits10"]) * n2 <= res["ties"] + 1e-6
+    assert abs(res["raw_hits10"] - ev["raw"]["hits10"]) * n2 <= res["ties"] + 1e-6
+
+
+def _random_transr(ds, n, seed, scale=0.3):
+    rng = np.random.default_rng(seed)
+    ent = rng.standard_normal((ds.num_entities, n))
+    ent /= np.linalg.norm(ent, axis=1, keepdims=True)
+    rel = rng.standard_normal((ds.num_relations, n)) * scale
+    w = np.eye(n)[None] + rng.standard_normal((ds.num_relations, n, n)) * (scale / np.sqrt(n))
+    return ent, rel, w
+
+
+@pytest.mark.parametrize("n,distance", [(20, 0), (50, 1), (100, 0), (128, 0)])
+def test_eval_transr_compat_tiny_dims(n, distance):
+    """n > 64: two and more elements per lane in the chain wave."""
+    ds = tiny()
+    ent, rel, w = _random_transr(ds, n, n)
+    _compat_vs_oracle(ds, n, ent, rel, w, distance=distance)
+
+
+def test_eval_transr_compat_small_set_with_state():
+    """2,000 entities (the per-relation cache on), 1,000 test triples over 40
+    relations, starting from non-zero work vectors (a process that already
+    evaluated something)."""
+    ds = data.synthetic("small", seed=5)
+    n = 20
+    ent, rel, w = _random_transr(ds, n, 1)
+    work = np.random.default_rng(2).standard_normal((2, n))
+    _compat_vs_oracle(ds, n, ent, rel, w, work=work)
+
+
+def test_eval_transr_compat_without_cache():
+    """|E| > 40,000 (common/evaluation.h:11): the reference evaluates with no cache,
+    every corruption recomputed."""
+    ds = data.synthetic("small", seed=6, counts=(40500, 3, 3000, 10, 12))
+    n = 8
+    ent, rel, w = _random_transr(ds, n, 3)
+    _compat_vs_oracle(ds, n, ent, rel, w)
+
+
+@pytest.mark.parametrize("model,dim", [("E", 200), ("H", 160)])
+def test_eval_wide_rows_matches_oracle(model, dim):
+    """dim > 128 (the reference accepts any --size)."""
+    ds = tiny()
+    rng = np.random.default_rng(dim)
+    ent = rng.standard_normal((ds.num_entities, dim)) * 0.1
+    rel = rng.standard_normal((ds.num_relations, dim)) * 0.1
+    w = None
+    if model == "H":
+        w = rng.standard_normal((ds.num_relations, dim))
+        w /= np.linalg.norm(w, axis=1, keepdims=True)
+    eng = Engine(model, dim, ds.num_entities, ds.num_relations)
+    eng.upload_params(ent, rel, w)
+    filt = np.concatenate([ds.test, ds.train, ds.valid])
+    res = eng.evaluate(ds.test, filt)
+    m = orc.Model(model, dim, ds.num_entities, ds.num_relations)
+    m.set_tables(ent, rel, w)
+    exp = m.evaluate(ds.test, filt)
+    for k in ("raw_rank", "raw_hits10", "filtered_rank", "filtered_hits10"):
+        assert res[k] == pytest.approx(exp[k], abs=1e-12), k
