@@ -208,6 +208,14 @@ kb2e_status kb2e_device_tables(kb2e_ctx* ctx, void** entity, void** relation, vo
  * relation. */
 kb2e_status kb2e_renormalize(kb2e_ctx* ctx, const uint8_t* entity_rows, const uint8_t* relation_rows,
                              const uint8_t* weight_rows);
+/* The same constraint on `count` units of one table from `first` (table 0:
+ * entities, 1: relations, 2: weights, in relations), with the row mask in
+ * DEVICE memory (device_mask[k] for unit first + k; NULL = every row), so a
+ * merge that computed the changed rows on the device never copies to the host
+ * (kb2e_amd/distributed.py: each rank renormalises the entity block it owns
+ * after a reduce-scatter). */
+kb2e_status kb2e_renormalize_rows(kb2e_ctx* ctx, int32_t table, int64_t first, int64_t count,
+                                  const uint8_t* device_mask);
 
 #ifdef __cplusplus
 }

@@ -997,6 +997,37 @@ __global__ __launch_bounds__(256) void renorm_kernel(T* table, int64_t rows, int
         v.store(table + r * ld, n);
     }
 }
+// The model's norm constraint on `count` units of a table from `first` (units:
+// entities, relations, or relations of the weights table), rows flagged in the
+// DEVICE mask (indexed from `first`; nullptr = all): TransE rows and TransH
+// entity/relation rows shrink to length <= 1 (common/utils.cpp:70-77), TransH
+// normals and TransR entity/relation/matrix rows are scaled to unit length
+// (transh/trainer.cpp:52, transr/trainer.cpp:174-180).  Asynchronous.
+void renorm_rows(kb2e_ctx* c, int table, int64_t first, int64_t count, const uint8_t* dmask) {
+    if (count <= 0) return;
+    const int model = c->cfg.model;
+    const bool unit = model == KB2E_TRANSR || table == 2;
+    DevBuf* t = table == 0 ? &c->ent : table == 1 ? &c->rel : &c->w;
+    const int div = model == KB2E_TRANSR && table == 2 ? c->n : 1;  // TransR: n matrix rows per relation
+    const int64_t rows = count * div;
+    const int64_t off = first * div * c->ld;
+    const int grid = (int)std::min<int64_t>((rows + 3) / 4, 65535);
+    auto go = [&](auto tag, auto chtag) {
+        using T = decltype(tag);
+        constexpr int CH = decltype(chtag)::value;
+        renorm_kernel<T, CH><<<grid, 256, 0, c->stream>>>(t->as<T>() + off, rows, c->ld, c->n, dmask, div, !unit);
+    };
+    if (c->f64()) {
+        if (c->ch == 1) go(double(), std::integral_constant<int, 1>());
+        else if (c->ch == 2) go(double(), std::integral_constant<int, 2>());
+        else go(double(), std::integral_constant<int, 4>());
+    } else {
+        if (c->ch == 1) go(float(), std::integral_constant<int, 1>());
+        else if (c->ch == 2) go(float(), std::integral_constant<int, 2>());
+        else go(float(), std::integral_constant<int, 4>());
+    }
+    HIPCHK(hipGetLastError());
+}
 }  // namespace
 
 // ================================================================== C ABI
@@ -1441,51 +1472,36 @@ kb2e_status kb2e_device_tables(kb2e_ctx* c, void** e, void** r, void** w, int64_
 kb2e_status kb2e_renormalize(kb2e_ctx* c, const uint8_t* ent_rows, const uint8_t* rel_rows, const uint8_t* w_rows) {
     return guarded(c, [&] {
         HIPCHK(hipSetDevice(c->cfg.device));
-        const int model = c->cfg.model;
-        // (table, rows, host mask, mask divisor, ignore_short)
-        struct Job {
-            DevBuf* t;
-            int64_t rows;
-            const uint8_t* mask;
-            int64_t mask_rows;
-            int div;
-            bool ignore_short;
-        };
-        std::vector<Job> jobs;
-        const bool unit = model == KB2E_TRANSR;
-        jobs.push_back({&c->ent, c->cfg.num_entities, ent_rows, c->cfg.num_entities, 1, !unit});
-        jobs.push_back({&c->rel, c->cfg.num_relations, rel_rows, c->cfg.num_relations, 1, !unit});
-        if (model == KB2E_TRANSH) jobs.push_back({&c->w, c->cfg.num_relations, w_rows, c->cfg.num_relations, 1, false});
-        if (model == KB2E_TRANSR)
-            jobs.push_back({&c->w, (int64_t)c->cfg.num_relations * c->n, w_rows, c->cfg.num_relations, c->n, false});
+        const uint8_t* masks[3] = {ent_rows, rel_rows, w_rows};
+        const int ntab = c->cfg.model == KB2E_TRANSE ? 2 : 3;
         DevBuf mbuf;
-        for (const Job& j : jobs) {
+        for (int t = 0; t < ntab; ++t) {
+            const int64_t units = t == 0 ? c->cfg.num_entities : c->cfg.num_relations;
             const uint8_t* dmask = nullptr;
-            if (j.mask) {
-                mbuf.alloc(j.mask_rows);
-                HIPCHK(hipMemcpyAsync(mbuf.p, j.mask, j.mask_rows, hipMemcpyHostToDevice, c->stream));
+            if (masks[t]) {
+                mbuf.alloc(units);
+                HIPCHK(hipMemcpyAsync(mbuf.p, masks[t], units, hipMemcpyHostToDevice, c->stream));
                 dmask = mbuf.as<uint8_t>();
             }
-            const int grid = (int)std::min<int64_t>((j.rows + 3) / 4, 65535);
-            auto go = [&](auto tag, auto chtag) {
-                using T = decltype(tag);
-                constexpr int CH = decltype(chtag)::value;
-                renorm_kernel<T, CH><<<grid, 256, 0, c->stream>>>(j.t->as<T>(), j.rows, c->ld, c->n, dmask, j.div,
-                                                                  j.ignore_short);
-            };
-            if (c->f64()) {
-                if (c->ch == 1) go(double(), std::integral_constant<int, 1>());
-                else if (c->ch == 2) go(double(), std::integral_constant<int, 2>());
-                else go(double(), std::integral_constant<int, 4>());
-            } else {
-                if (c->ch == 1) go(float(), std::integral_constant<int, 1>());
-                else if (c->ch == 2) go(float(), std::integral_constant<int, 2>());
-                else go(float(), std::integral_constant<int, 4>());
-            }
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipStreamSynchronize(c->stream));
+            renorm_rows(c, t, 0, units, dmask);
+            HIPCHK(hipStreamSynchronize(c->stream));  // mbuf is reused
         }
         sync_wsnap(c);
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_renormalize_rows(kb2e_ctx* c, int32_t table, int64_t first, int64_t count,
+                                  const uint8_t* device_mask) {
+    return guarded(c, [&] {
+        const int ntab = c->cfg.model == KB2E_TRANSE ? 2 : 3;
+        if (table < 0 || table >= ntab) return fail(c, KB2E_EINVAL, "no such table");
+        const int64_t units = table == 0 ? c->cfg.num_entities : c->cfg.num_relations;
+        if (first < 0 || count < 0 || first + count > units) return fail(c, KB2E_EINVAL, "rows out of range");
+        HIPCHK(hipSetDevice(c->cfg.device));
+        renorm_rows(c, table, first, count, device_mask);
+        if (table == 2) sync_wsnap(c);
+        else HIPCHK(hipStreamSynchronize(c->stream));
         return KB2E_OK;
     });
 }

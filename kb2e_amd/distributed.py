@@ -2,16 +2,26 @@
 
 SURVEY.md 8(e): every rank trains the triples whose head entity hashes to it
 (sampling only from its shard, with the reference's per-batch semantics on a
-full replica of the tables).  At each epoch boundary the ranks exchange their
-table deltas with one all-reduce (sum) over RCCL and re-apply the reference's
-norm constraints (kb2e_renormalize):
+full replica of the tables).  At each epoch boundary the ranks merge their
+table deltas and re-apply the reference's norm constraints:
 
     T <- renorm(T0 + sum_r (T_r - T0))
 
-Rows touched by one rank get exactly that rank's update; shared rows (popular
-relations) get every rank's contribution, like a sequential pass over the
-shards.  This is a documented relaxation of the single-GPU semantics (local
-SGD per epoch); single-GPU runs are exact.
+* relations and the relation weights (TransH normals, TransR matrices): one
+  all-reduce (sum) of the deltas over RCCL, then every rank renormalises the
+  rows any rank changed (the same rows on every rank: the summed delta is the
+  same everywhere);
+* entities: a reduce-scatter of the deltas to the owner of each contiguous
+  block of rows, the owner adds them, renormalises its changed rows, and an
+  all-gather hands every rank the merged table -- the all-reduce's bytes, but
+  each rank renormalises only 1/N of the rows.
+
+The changed-row masks are computed and consumed on the device
+(kb2e_renormalize_rows takes a device mask): no host copy, no host sync beyond
+the collectives themselves.  Rows touched by one rank get exactly that rank's
+update; shared rows (popular relations) get every rank's contribution, like a
+sequential pass over the shards.  This is a documented relaxation of the
+single-GPU semantics (local SGD per epoch); single-GPU runs are exact.
 """
 from __future__ import annotations
 
@@ -48,51 +58,119 @@ def engine_tables(eng):
     return out
 
 
-def merge_deltas(tables, base, dist, row_len):
-    """In place: tables <- base + all_reduce_sum(tables - base).  Returns, per
-    table, a uint8 mask of the rows any rank changed (numpy, for renormalize)."""
-    masks = []
-    for t, b, rl in zip(tables, base, row_len):
-        t.sub_(b)
-        dist.all_reduce(t)
-        masks.append((t.view(-1, rl) != 0).any(dim=1).to("cpu").numpy().astype(np.uint8))
-        t.add_(b)
-    while len(masks) < 3:
-        masks.append(None)
-    return masks
+class _EngineRows:
+    """The norm constraint of a live engine on a row range (device mask)."""
 
-
-class EpochMerger:
-    """Epoch-boundary exchange for one engine (rank)."""
-
-    def __init__(self, eng, dist):
+    def __init__(self, eng):
         self.eng = eng
-        self.dist = dist
-        self.tables = engine_tables(eng)
-        # all ranks start from rank 0's tables
-        eng.synchronize()
-        for t in self.tables:
+
+    def synchronize(self):
+        self.eng.synchronize()
+
+    def renormalize(self, table, first, count, mask):
+        import torch
+
+        torch.cuda.synchronize()  # torch's stream wrote the rows; the engine's stream renormalises them
+        self.eng.renormalize_rows(table, first, count, mask.data_ptr() if mask is not None else None)
+
+
+def _host_staged(dist, t):
+    """gloo over device tensors (the one-GPU rehearsal, tests/test_gpu_distributed.py)
+    runs these collectives through host copies."""
+    return t.is_cuda and dist.get_backend() == "gloo"
+
+
+def _reduce_scatter(dist, out, inp):
+    if _host_staged(dist, inp):
+        o = out.cpu()
+        dist.reduce_scatter_tensor(o, inp.cpu())
+        out.copy_(o)
+    else:
+        dist.reduce_scatter_tensor(out, inp)
+
+
+def _all_gather(dist, out, inp):
+    if _host_staged(dist, inp):
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu())
+        out.copy_(o)
+    else:
+        dist.all_gather_into_tensor(out, inp)
+
+
+def _changed(delta, row_len):
+    """uint8 mask of the rows with a non-zero delta (on the tensor's device)."""
+    import torch
+
+    return (delta.view(-1, row_len) != 0).any(dim=1).to(torch.uint8)
+
+
+class TableMerger:
+    """The epoch-boundary exchange over tables given as flat tensors.
+
+    tables: [entity, relation(, weights)] flat tensors (views of the engine's
+    memory on a GPU; plain tensors in the CPU tests); units: rows per table
+    (entities, relations, relations); unit_len: elements per unit;
+    rows: an object with renormalize(table, first, count, mask) and
+    synchronize()."""
+
+    def __init__(self, tables, units, unit_len, rows, dist):
+        import torch
+
+        self.tables, self.units, self.unit_len, self.rows, self.dist = tables, units, unit_len, rows, dist
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        rows.synchronize()
+        for t in tables:  # every rank starts from rank 0's tables
             dist.broadcast(t, 0)
-        self.base = [t.clone() for t in self.tables]
+        self.base = [t.clone() for t in tables]
+        ne, L = units[0], unit_len[0]
+        self.block = (ne + self.world - 1) // self.world  # entity rows per owner
+        self.lo = min(ne, self.rank * self.block)
+        self.hi = min(ne, self.lo + self.block)
+        dev, dt = tables[0].device, tables[0].dtype
+        self.send = torch.zeros(self.block * self.world * L, dtype=dt, device=dev)
+        self.recv = torch.zeros(self.block * L, dtype=dt, device=dev)
 
     def merge(self):
         import torch
 
-        self.eng.synchronize()
-        masks = merge_deltas(self.tables, self.base, self.dist, self.row_lengths())
-        torch.cuda.synchronize()
-        self.eng.renormalize(*masks)
-        self.eng.synchronize()
+        self.rows.synchronize()
+        ne, L = self.units[0], self.unit_len[0]
+        ent, base = self.tables[0], self.base[0]
+        # entities: reduce-scatter the deltas to the block owners
+        torch.sub(ent, base, out=self.send[: ne * L])
+        _reduce_scatter(self.dist, self.recv, self.send)
+        n_own = self.hi - self.lo
+        own = ent[self.lo * L: self.hi * L]
+        torch.add(base[self.lo * L: self.hi * L], self.recv[: n_own * L], out=own)
+        if n_own:
+            mask = _changed(self.recv[: n_own * L], L)
+            self.rows.renormalize(0, self.lo, n_own, mask)
+        self.recv[: n_own * L].copy_(own)
+        _all_gather(self.dist, self.send, self.recv)
+        ent.copy_(self.send[: ne * L])
+        # relations and weights: all-reduce the deltas, every rank renormalises
+        for k in range(1, len(self.tables)):
+            t, b = self.tables[k], self.base[k]
+            t.sub_(b)
+            self.dist.all_reduce(t)
+            mask = _changed(t, self.unit_len[k])
+            t.add_(b)
+            self.rows.renormalize(k, 0, self.units[k], mask)
+        self.rows.synchronize()
         for t, b in zip(self.tables, self.base):
             b.copy_(t)
 
-    def row_lengths(self):
-        """Elements per mask row of each table (weights: one mask row per relation)."""
-        ld = self.tables[0].numel() // self.eng.ne
-        out = [ld, ld]
-        if len(self.tables) > 2:
-            out.append(self.tables[2].numel() // self.eng.nr)
-        return out
+
+class EpochMerger(TableMerger):
+    """TableMerger over a live engine's device tables (one engine per rank)."""
+
+    def __init__(self, eng, dist):
+        tables = engine_tables(eng)
+        ld = tables[0].numel() // eng.ne
+        units = [eng.ne, eng.nr] + ([eng.nr] if len(tables) > 2 else [])
+        unit_len = [ld, ld] + ([tables[2].numel() // eng.nr] if len(tables) > 2 else [])
+        super().__init__(tables, units, unit_len, _EngineRows(eng), dist)
 
 
 def shard_heads(triples: np.ndarray, rank: int, world: int) -> np.ndarray:

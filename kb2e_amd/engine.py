@@ -26,6 +26,7 @@ EXPORTS = [
     "kb2e_set_transr_work", "kb2e_set_sample_stream", "kb2e_get_sample_stream", "kb2e_train_epoch", "kb2e_train_batches",
     "kb2e_synchronize", "kb2e_take_stats", "kb2e_rng_next", "kb2e_profile_enable", "kb2e_profile_query",
     "kb2e_device_bytes", "kb2e_device_tables", "kb2e_renormalize", "kb2e_evaluate", "kb2e_evaluate_transr_compat",
+    "kb2e_renormalize_rows",
 ]
 
 
@@ -74,6 +75,7 @@ def lib():
             "kb2e_device_tables": (i32, [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(i64),
                                          C.POINTER(i64), C.POINTER(i64)]),
             "kb2e_renormalize": (i32, [vp, u8p, u8p, u8p]),
+            "kb2e_renormalize_rows": (i32, [vp, i32, i64, i64, vp]),
             "kb2e_evaluate": (i32, [vp, i32p, i32p, i32p, i64, i32p, i32p, i32p, i64, dp]),
             "kb2e_evaluate_transr_compat": (i32, [vp, i32p, i32p, i32p, i64, i32p, i32p, i32p, i64, dp, dp, vp,
                                                   vp]),
@@ -228,6 +230,11 @@ class Engine:
         keep = [None if m is None else np.ascontiguousarray(m, dtype=np.uint8) for m in (ent_rows, rel_rows, w_rows)]
         ptrs = [None if m is None else m.ctypes.data_as(C.POINTER(C.c_uint8)) for m in keep]
         self._check(lib().kb2e_renormalize(self.h, *ptrs), "renormalize")
+
+    def renormalize_rows(self, table, first, count, device_mask_ptr=None):
+        """Norm constraint on rows [first, first + count) of table 0/1/2, mask in device memory."""
+        self._check(lib().kb2e_renormalize_rows(self.h, int(table), int(first), int(count), device_mask_ptr),
+                    "renormalize_rows")
 
     def evaluate(self, test, filt):
         """Link prediction (raw/filtered mean rank and hits@10) on the device tables."""

@@ -1,6 +1,7 @@
-"""Multi-rank path on CPU (gloo, world size 2): head-hash sharding and the
-epoch-boundary delta merge of kb2e_amd.distributed."""
-import os
+"""Multi-rank path on CPU (gloo, world size 2 and 3): head-hash sharding and the
+epoch-boundary merge of kb2e_amd.distributed (reduce-scatter of entity deltas
+to block owners + all-gather, all-reduce of relation/weight deltas, changed
+rows renormalised) against numpy renorm(T0 + sum_r (T_r - T0))."""
 import socket
 
 import numpy as np
@@ -10,7 +11,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from kb2e_amd import data
-from kb2e_amd.distributed import merge_deltas, shard_heads
+from kb2e_amd.distributed import TableMerger, shard_heads
 
 
 def _free_port():
@@ -30,32 +31,84 @@ def test_shards_partition_the_triples():
     assert min(len(p) for p in parts) > 0.15 * len(ds.train)
 
 
+NE, NR, L = 11, 4, 3  # 11 entity rows: uneven blocks over 2 and 3 ranks
+
+
+class CpuRows:
+    """The engine's row constraint on CPU tensors: shrink rows longer than 1
+    (TransE, common/utils.cpp:70-77) -- unit length for the weights (TransH w)."""
+
+    def __init__(self, tables):
+        self.tables = tables
+        self.calls = []
+
+    def synchronize(self):
+        pass
+
+    def renormalize(self, table, first, count, mask):
+        t = self.tables[table].view(-1, L)[first:first + count]
+        self.calls.append((table, first, count))
+        for k in range(count):
+            if mask is not None and not mask[k]:
+                continue
+            n = float(torch.sqrt((t[k] ** 2).sum()))
+            if table == 2 or n > 1:
+                t[k] /= n
+
+
+def _initial():
+    rng = np.random.default_rng(0)
+    return [rng.uniform(-0.5, 0.5, (NE, L)), rng.uniform(-0.5, 0.5, (NR, L)), rng.uniform(-1, 1, (NR, L))]
+
+
+def _rank_update(rank):
+    """What rank `rank` trained: a few entity rows (some shared), a shared relation, a weight row."""
+    rng = np.random.default_rng(100 + rank)
+    d = [np.zeros((NE, L)), np.zeros((NR, L)), np.zeros((NR, L))]
+    for e in {rank, rank + 3, 7, NE - 1}:
+        d[0][e] = rng.normal(0, 0.8, L)
+    d[1][1] = rng.normal(0, 0.8, L)
+    d[2][rank % NR] = rng.normal(0, 0.3, L)
+    return d
+
+
 def _worker(rank, world, port, out):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    rows, ld = 6, 4
-    base = [torch.arange(rows * ld, dtype=torch.float64) / 10.0, torch.ones(3 * ld, dtype=torch.float64)]
-    tables = [b.clone() for b in base]
-    # rank r updates entity row r and relation row 0 (shared)
-    tables[0].view(rows, ld)[rank] += rank + 1
-    tables[1].view(3, ld)[0] += 0.5
-    masks = merge_deltas(tables, base, dist, [ld, ld])
-    out[rank] = (tables[0].numpy().copy(), tables[1].numpy().copy(), masks[0].copy(), masks[1].copy())
+    init = _initial()
+    # rank 0's tables win the initial broadcast: others start from garbage
+    tables = [torch.tensor(t if rank == 0 else t + 5.0).reshape(-1) for t in init]
+    rows = CpuRows(tables)
+    m = TableMerger(tables, [NE, NR, NR], [L, L, L], rows, dist)
+    for t, d in zip(tables, _rank_update(rank)):
+        t += torch.tensor(d).reshape(-1)
+    m.merge()
+    out[rank] = ([t.numpy().copy() for t in tables], rows.calls)
     dist.destroy_process_group()
 
 
 @pytest.mark.timeout(120)
-def test_merge_sums_rank_deltas_gloo():
-    world = 2
+@pytest.mark.parametrize("world", [2, 3])
+def test_merge_matches_numpy_renorm_of_summed_deltas(world):
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
-    base_e = np.arange(24, dtype=np.float64).reshape(6, 4) / 10.0
-    exp_e = base_e.copy()
-    exp_e[0] += 1
-    exp_e[1] += 2
-    exp_r = np.ones((3, 4))
-    exp_r[0] += 1.0  # both ranks' +0.5
+    init = _initial()
+    exp = [t.copy() for t in init]
+    changed = [np.zeros(len(t), bool) for t in init]
     for r in range(world):
-        e, rel, me, mr = out[r]
-        assert np.allclose(e.reshape(6, 4), exp_e) and np.allclose(rel.reshape(3, 4), exp_r)
-        assert me.tolist() == [1, 1, 0, 0, 0, 0] and mr.tolist() == [1, 0, 0]
+        for k, d in enumerate(_rank_update(r)):
+            exp[k] += d
+            changed[k] |= (d != 0).any(1)
+    for k, t in enumerate(exp):
+        for i in np.nonzero(changed[k])[0]:
+            n = np.linalg.norm(t[i])
+            if k == 2 or n > 1:
+                t[i] /= n
+    block = (NE + world - 1) // world
+    for r in range(world):
+        tabs, calls = out[r]
+        for k in range(3):
+            assert np.allclose(tabs[k].reshape(-1, L), exp[k], atol=1e-12), (r, k)
+        # each rank renormalised only its own entity block
+        lo = min(NE, r * block)
+        assert (0, lo, min(NE, lo + block) - lo) in calls

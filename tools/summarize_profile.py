@@ -46,7 +46,42 @@ def phase(name):
     return None
 
 
-def main(src, tag, config, prec, schedule="parallel", batches="120"):
+PEAK_F64_MFMA_TFLOPS = 78.6  # v_mfma_f64_16x16x4_f64: 64 cycles / 2048 FLOP per SIMD, 1024 SIMDs, 2.4 GHz
+
+
+def mfma_table(src, stats):
+    """f64 MFMA work and utilisation per kernel from the SQ_INSTS_VALU_MFMA_MOPS_F64
+    / SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE pass (rocprofv3 derived-counter
+    formulas: MfmaFlopsF64 = MOPS_F64 x 512, MfmaUtil = BUSY / (GUI_ACTIVE x SIMDs))."""
+    path = os.path.join(src, "pmc_MFMA", "run_counter_collection.csv")
+    if not os.path.exists(path):
+        return {}
+    agg = defaultdict(lambda: defaultdict(float))
+    cnt = defaultdict(lambda: defaultdict(int))
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"].split("(")[0].split("<")[0].strip()
+        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        cnt[k][r["Counter_Name"]] += 1
+    avg_us = {r["Name"].split("(")[0].split("<")[0].strip(): float(r["AverageNs"]) / 1e3 for r in stats}
+    out = {}
+    for k, v in agg.items():
+        n = max(cnt[k].values())
+        mops = v.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0) / n
+        if mops <= 0:
+            continue
+        flops = mops * 512
+        busy = v.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / n
+        gui = v.get("GRBM_GUI_ACTIVE", 0.0) / n
+        us = avg_us.get(k)
+        out[k] = {"mfma_f64_flop_per_launch": flops, "avg_us": us,
+                  "achieved_tflops": flops / (us * 1e-6) / 1e12 if us else None,
+                  "frac_of_f64_mfma_peak": (flops / (us * 1e-6) / 1e12) / PEAK_F64_MFMA_TFLOPS if us else None,
+                  "mfma_busy_cycles": busy, "gui_active_cycles": gui,
+                  "mfma_util_pct": 100.0 * busy / (gui * 1024) if gui else None}
+    return out
+
+
+def main(src, tag, config, prec, schedule="parallel", batches="200"):
     nbatch = float(batches)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
@@ -63,6 +98,8 @@ def main(src, tag, config, prec, schedule="parallel", batches="120"):
             a[0] += float(r["Counter_Value"])
             a[1] += 1
             p = phase(r["Kernel_Name"])
+            if config.startswith("transr") and ("transe_" in r["Kernel_Name"] or "long_segments" in r["Kernel_Name"]):
+                p = None  # the TransE-init seed run of bench.py, not the measured TransR batches
             for q in (p.split("|") if p else []):
                 ph[q] += float(r["Counter_Value"])
         pmc[c] = {k: v[0] / max(1, v[1]) for k, v in agg.items()}  # KiB per launch
@@ -77,6 +114,9 @@ def main(src, tag, config, prec, schedule="parallel", batches="120"):
         w = pmc.get("WRITE_SIZE_phase", {}).get(p, 0.0) * 1024
         per_kernel[p] = {"fetch_bytes_raw": f, "write_bytes": w, "hbm_bytes_per_launch": 2 * f + w,
                          "note": "phase total per batch"}
+    mf = mfma_table(src, stats)
+    if mf:
+        per_kernel["mfma_f64"] = mf
     out_json = os.path.join(root, "profiles", f"pmc_{config}_{schedule}_f{prec}.json")
     json.dump(per_kernel, open(out_json, "w"), indent=1, sort_keys=True)
     lines = [f"# Profile {tag}: {config}, {schedule} schedule (f{prec})", "", "Command: `tools/gpu_profile.sh` on one MI355X "
@@ -88,8 +128,16 @@ def main(src, tag, config, prec, schedule="parallel", batches="120"):
                      f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} |")
     lines += ["", "## HBM traffic per launch (PMC, gfx950-corrected: 2 x FETCH_SIZE + WRITE_SIZE)", "",
               "| kernel family | FETCH_SIZE raw (bytes) | WRITE_SIZE (bytes) | corrected HBM bytes |", "|---|---|---|---|"]
-    for fam, v in sorted(per_kernel.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"])[:12]:
+    for fam, v in sorted(((k, v) for k, v in per_kernel.items() if k != "mfma_f64"),
+                         key=lambda kv: -kv[1]["hbm_bytes_per_launch"])[:12]:
         lines.append(f"| {fam} | {v['fetch_bytes_raw']:.0f} | {v['write_bytes']:.0f} | {v['hbm_bytes_per_launch']:.0f} |")
+    if mf:
+        lines += ["", f"## f64 MFMA per launch (PMC: SQ_INSTS_VALU_MFMA_MOPS_F64 x 512; peak {PEAK_F64_MFMA_TFLOPS} TF)", "",
+                  "| kernel | MFMA FLOP | avg us | TFLOP/s | frac of f64 MFMA peak | MfmaUtil % |", "|---|---|---|---|---|---|"]
+        for k, v in sorted(mf.items(), key=lambda kv: -kv[1]["mfma_f64_flop_per_launch"]):
+            lines.append(f"| {k[:50]} | {v['mfma_f64_flop_per_launch']:.3g} | {v['avg_us'] or 0:.1f} | "
+                         f"{v['achieved_tflops'] or 0:.2f} | {v['frac_of_f64_mfma_peak'] or 0:.4f} | "
+                         f"{v['mfma_util_pct'] or 0:.2f} |")
     md = os.path.join(root, "profiles", f"{tag}_{config}_{schedule}_f{prec}.md")
     open(md, "w").write("\n".join(lines) + "\n")
     print(md, out_json)
