@@ -6,21 +6,27 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -Wall -Iinclude
 
-CSRC := $(filter-out kb2e_amd/csrc/eval.hip,$(wildcard kb2e_amd/csrc/*.hip kb2e_amd/csrc/*.hpp kb2e_amd/csrc/*.inc)) include/kb2e_engine.h
+CSRC := $(filter-out kb2e_amd/csrc/eval.hip kb2e_amd/csrc/textio.hip,$(wildcard kb2e_amd/csrc/*.hip kb2e_amd/csrc/*.hpp kb2e_amd/csrc/*.inc)) include/kb2e_engine.h
 
 BINS := bin/trainTransE bin/trainTransH bin/trainTransR bin/evalTransE bin/evalTransH bin/evalTransR
 
-all: kb2e_amd/libkb2e.so bin/kb2e $(BINS) oracle
+all: kb2e_amd/libkb2e.so bin/kb2e $(BINS) oracle bin/textio_check
 
 bin/kb2e: kb2e_amd/csrc/host/kb2e_cli.cpp include/kb2e_engine.h kb2e_amd/libkb2e.so
 	@mkdir -p bin
 	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ kb2e_amd/csrc/host/kb2e_cli.cpp -Lkb2e_amd -lkb2e \
 	    -Wl,-rpath,'$$ORIGIN/../kb2e_amd'
 
+# host check of the shared formatter / parser against glibc (tests/test_textio.py)
+bin/textio_check: tests/native/textio_check.cpp kb2e_amd/csrc/textio.hpp
+	@mkdir -p bin
+	g++ -O2 -std=c++17 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -o $@ tests/native/textio_check.cpp
+
 $(BINS): bin/kb2e
 	ln -sf kb2e $@
 
-# two translation units (the training engine, the evaluator), compiled in parallel
+# three translation units (the training engine, the evaluator, text I/O + device
+# init), compiled in parallel
 kb2e_amd/build/engine.o: $(CSRC)
 	@mkdir -p kb2e_amd/build
 	$(HIPCC) $(HIPFLAGS) -c -o $@ kb2e_amd/csrc/engine.hip
@@ -30,14 +36,20 @@ kb2e_amd/build/eval.o: kb2e_amd/csrc/eval.hip kb2e_amd/csrc/eval.hpp kb2e_amd/cs
 	@mkdir -p kb2e_amd/build
 	$(HIPCC) $(HIPFLAGS) -c -o $@ kb2e_amd/csrc/eval.hip
 
-kb2e_amd/libkb2e.so: kb2e_amd/build/engine.o kb2e_amd/build/eval.o
+kb2e_amd/build/textio.o: kb2e_amd/csrc/textio.hip kb2e_amd/csrc/textio.hpp kb2e_amd/csrc/hip_util.hpp \
+		kb2e_amd/csrc/kernels_glibc.hpp kb2e_amd/csrc/glibc_rand.hpp
+	@mkdir -p kb2e_amd/build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ kb2e_amd/csrc/textio.hip
+
+kb2e_amd/libkb2e.so: kb2e_amd/build/engine.o kb2e_amd/build/eval.o kb2e_amd/build/textio.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 # diagnostic build: per-phase cycle counters in the relation-owner kernels
 prof: kb2e_amd/libkb2e_prof.so
 
-kb2e_amd/libkb2e_prof.so: $(CSRC) kb2e_amd/build/eval.o
-	$(HIPCC) $(HIPFLAGS) -DKB2E_OWNER_PROF -shared -o $@ kb2e_amd/csrc/engine.hip kb2e_amd/build/eval.o
+kb2e_amd/libkb2e_prof.so: $(CSRC) kb2e_amd/build/eval.o kb2e_amd/build/textio.o
+	$(HIPCC) $(HIPFLAGS) -DKB2E_OWNER_PROF -shared -o $@ kb2e_amd/csrc/engine.hip kb2e_amd/build/eval.o \
+	    kb2e_amd/build/textio.o
 
 oracle:
 	$(MAKE) -C oracle all

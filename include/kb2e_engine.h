@@ -112,6 +112,35 @@ kb2e_status kb2e_init_params(kb2e_ctx* ctx, double* entity, double* relation, do
  * that kb2e_init_params set.  Call after kb2e_init_params. */
 kb2e_status kb2e_transr_seed(kb2e_ctx* ctx, const double* entity, const double* relation);
 
+/* Trainer::prepTrain's draws made on the device: the same
+ * randn values (common/utils.cpp:26-38), row norms and TransH / TransR weight
+ * init as kb2e_init_params, taken from the same glibc stream and leaving it at
+ * the same position -- the epochs that follow are unchanged.  Every rejection
+ * attempt is evaluated in parallel (the stream is made on the device from the
+ * generator's 31-word window) and the accepted ones are compacted in order.
+ * *near_ties (may be NULL) = accept/reject decisions within a few ulps of the
+ * density, where the device exp and glibc's could round differently. */
+kb2e_status kb2e_init_params_device(kb2e_ctx* ctx, double* entity, double* relation, double* weights,
+                                    int64_t* near_ties);
+
+/* Text tables.  table: 0 entities (|E| rows), 1 relations
+ * (|R| rows), 2 weights (TransH |R| rows, TransR |R|*n rows).
+ * kb2e_write_table writes the device table as Trainer::write does
+ * (common/trainer.cpp:109-127, transh/trainer.cpp:94-105,
+ * transr/trainer.cpp:128-142): "%.6lf\t" per value, "\n" per row, formatted
+ * on the device byte for byte as glibc printf; kb2e_format_table returns the
+ * same bytes in `buf` (*len = the length needed; KB2E_EINVAL if cap is short).
+ * kb2e_read_table loads a table from "%lf" text as the TransR seed step reads
+ * its files (transr/trainer.cpp:88-113): whitespace-separated tokens, the first
+ * rows*n used, converted on the device (correctly rounded, as strtod), then
+ * optionally normalised per row.  KB2E_EINVAL with the reference's message when
+ * the file holds fewer numbers. */
+enum { KB2E_READ_VERBATIM = 0, KB2E_READ_UNIT = 1 /* common::norm(row, false) */,
+       KB2E_READ_SHRINK = 2 /* common::norm(row): only rows longer than 1 */ };
+kb2e_status kb2e_write_table(kb2e_ctx* ctx, int32_t table, const char* path);
+kb2e_status kb2e_format_table(kb2e_ctx* ctx, int32_t table, char* buf, int64_t cap, int64_t* len);
+kb2e_status kb2e_read_table(kb2e_ctx* ctx, int32_t table, const char* path, int32_t mode);
+
 /* Upload tables (row-major FP64 as in the reference's vectors).  `weights` may
  * be NULL for TransE.  Used for TransR seeding (transr/trainer.cpp:88-113; the
  * caller applies the entity unit norm as the reference does) and for restarts. */

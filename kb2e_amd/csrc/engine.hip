@@ -39,6 +39,7 @@
 #include "kernels_transr_parallel.hpp"
 #include "kernels_transr_mfma.hpp"
 #include "kernels_transh_parallel.hpp"
+#include "textio.hpp"
 
 using namespace kb2e;
 
@@ -81,6 +82,7 @@ struct kb2e_ctx {
     GlibcRand rng{1};
     TripleStore ts;
     bool have_triples = false, have_params = false;
+    int tables_read = 0;  // kb2e_read_table: bit t = table t loaded from text
     int n = 0, ld = 0, ch = 1, nw = 2, esize = 8;
     int64_t B = 0, nb = 0, S = 0;
     hipStream_t stream = nullptr;
@@ -438,6 +440,15 @@ void ensure_sampler_capacity(kb2e_ctx* c, int64_t nraw) {
     c->nraw_cap = nraw;
 }
 
+// The glibc jump table (glibc_rand.hpp) on the device, made once per context.
+void ensure_jump_table(kb2e_ctx* c) {
+    if (c->glibc_table.p) return;
+    std::vector<uint32_t> C((size_t)GlibcRand::kDeg * kGlibcBlock);
+    glibc_jump_table(kGlibcBlock, C.data());
+    c->glibc_table.alloc(C.size() * 4);
+    HIPCHK(hipMemcpy(c->glibc_table.p, C.data(), C.size() * 4, hipMemcpyHostToDevice));
+}
+
 // Draw the stream of the epoch that follows the committed rng state into set
 // cur^1, on the side stream: the device makes the epoch's raw glibc words from
 // the generator's 31-word window (jump table, kernels_sampler.hpp) and resolves
@@ -447,12 +458,7 @@ void launch_prefetch(kb2e_ctx* c) {
     const int64_t nraw = (int64_t)(c->words_per_sample * c->S) + 4096;
     ensure_sampler_capacity(c, nraw);
     c->nraw = nraw;
-    if (!c->glibc_table.p) {
-        std::vector<uint32_t> C((size_t)GlibcRand::kDeg * kGlibcBlock);
-        glibc_jump_table(kGlibcBlock, C.data());
-        c->glibc_table.alloc(C.size() * 4);
-        HIPCHK(hipMemcpy(c->glibc_table.p, C.data(), C.size() * 4, hipMemcpyHostToDevice));
-    }
+    ensure_jump_table(c);
     GlibcWindow win;
     c->rng.window(win.w);
     hipStream_t st = c->side_stream;
@@ -1191,6 +1197,36 @@ kb2e_status kb2e_init_params(kb2e_ctx* c, double* ent_out, double* rel_out, doub
     });
 }
 
+kb2e_status kb2e_init_params_device(kb2e_ctx* c, double* ent_out, double* rel_out, double* w_out,
+                                    int64_t* near_ties) {
+    return guarded(c, [&] {
+        HIPCHK(hipSetDevice(c->cfg.device));
+        ensure_jump_table(c);
+        const int n = c->n, model = c->cfg.model;
+        const int64_t ne = c->cfg.num_entities, nr = c->cfg.num_relations;
+        // common/trainer.cpp:45-57 relations then entities; transh/trainer.cpp:80-87 then the normals
+        const int64_t rows = nr + ne + (model == KB2E_TRANSH ? nr : 0);
+        DevBuf vals;
+        vals.alloc((size_t)rows * n * 8);
+        // initialEmbeddingValue: transe/trainer.cpp:21-23, transh/trainer.cpp:61-63, transr/trainer.cpp:66-68
+        const double lim = model == KB2E_TRANSE ? 6 / std::sqrt((double)n) : 1.0;
+        const int64_t ties = device_randn(c->rng, c->glibc_table.as<uint32_t>(), kGlibcBlock, 0, 1.0 / n, -lim, lim,
+                                          rows * n, vals.as<double>(), c->stream);
+        c->rng_version++;
+        const double* v = vals.as<double>();
+        place_rows(v, nr, n, c->ld, c->rel.p, c->f64(), true, true, c->stream);
+        place_rows(v + nr * n, ne, n, c->ld, c->ent.p, c->f64(), true, true, c->stream);
+        if (model == KB2E_TRANSH) place_rows(v + (nr + ne) * n, nr, n, c->ld, c->w.p, c->f64(), true, false, c->stream);
+        if (model == KB2E_TRANSR) identity_weights(c->w.p, nr, n, c->ld, c->f64(), c->stream);
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (model == KB2E_TRANSR) sync_wsnap(c);
+        c->have_params = true;
+        if (near_ties) *near_ties = ties;
+        if (ent_out || rel_out || w_out) return kb2e_download_params(c, ent_out, rel_out, w_out);
+        return KB2E_OK;
+    });
+}
+
 kb2e_status kb2e_transr_seed(kb2e_ctx* c, const double* e, const double* r) {
     return guarded(c, [&] {
         if (c->cfg.model != KB2E_TRANSR) return fail(c, KB2E_EUNSUPPORTED, "TransR only");
@@ -1217,6 +1253,84 @@ kb2e_status kb2e_upload_params(kb2e_ctx* c, const double* e, const double* r, co
             return fail(c, KB2E_EINVAL, "entity, relation (and weight) tables required");
         upload_tables(c, e, r, w);
         c->have_params = true;
+        return KB2E_OK;
+    });
+}
+
+// ------------------------------------------------ text tables
+
+namespace {
+DevBuf* table_buf(kb2e_ctx* c, int32_t table, int64_t& rows) {
+    rows = table == 0 ? c->cfg.num_entities : table == 1 ? c->cfg.num_relations : w_rows(c);
+    if (table < 0 || table > 2 || rows == 0) throw std::invalid_argument("no such table for this model");
+    return table == 0 ? &c->ent : table == 1 ? &c->rel : &c->w;
+}
+}  // namespace
+
+kb2e_status kb2e_format_table(kb2e_ctx* c, int32_t table, char* buf, int64_t cap, int64_t* len) {
+    return guarded(c, [&] {
+        HIPCHK(hipSetDevice(c->cfg.device));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        int64_t rows = 0;
+        DevBuf* t = table_buf(c, table, rows);
+        int64_t at = 0;
+        const int64_t total = format_table(t->p, c->f64(), rows, c->n, c->ld, c->stream,
+                                           [&](const char* p, size_t k) {
+                                               if (buf && at + (int64_t)k <= cap) std::memcpy(buf + at, p, k);
+                                               at += (int64_t)k;
+                                           });
+        if (len) *len = total;
+        if (!buf || total > cap) return fail(c, KB2E_EINVAL, "buffer too small for the formatted table");
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_write_table(kb2e_ctx* c, int32_t table, const char* path) {
+    return guarded(c, [&] {
+        HIPCHK(hipSetDevice(c->cfg.device));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        int64_t rows = 0;
+        DevBuf* t = table_buf(c, table, rows);
+        FILE* f = path ? std::fopen(path, "w") : nullptr;
+        if (!f) return fail(c, KB2E_EINVAL, std::string("could not open output file: ") + (path ? path : "(null)"));
+        bool ok = true;
+        format_table(t->p, c->f64(), rows, c->n, c->ld, c->stream,
+                     [&](const char* p, size_t k) { ok = ok && std::fwrite(p, 1, k, f) == k; });
+        ok = (std::fclose(f) == 0) && ok;
+        if (!ok) return fail(c, KB2E_EINVAL, std::string("write failed: ") + path);
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_read_table(kb2e_ctx* c, int32_t table, const char* path, int32_t mode) {
+    return guarded(c, [&] {
+        HIPCHK(hipSetDevice(c->cfg.device));
+        if (mode < KB2E_READ_VERBATIM || mode > KB2E_READ_SHRINK) return fail(c, KB2E_EINVAL, "bad read mode");
+        int64_t rows = 0;
+        DevBuf* t = table_buf(c, table, rows);
+        FILE* f = path ? std::fopen(path, "rb") : nullptr;
+        if (!f) return fail(c, KB2E_EINVAL, std::string("could not open table file: ") + (path ? path : "(null)"));
+        std::vector<char> text;
+        char chunk[1 << 16];
+        size_t k;
+        while ((k = std::fread(chunk, 1, sizeof chunk, f)) > 0) text.insert(text.end(), chunk, chunk + k);
+        std::fclose(f);
+        const int64_t count = rows * c->n;
+        DevBuf vals;
+        vals.alloc((size_t)count * 8);
+        HIPCHK(hipStreamSynchronize(c->stream));
+        int64_t bad = -1, slow = 0;
+        const int64_t got = parse_doubles(text.data(), (int64_t)text.size(), count, vals.as<double>(), c->stream,
+                                          &bad, &slow);
+        if (got < count)
+            return fail(c, KB2E_EINVAL, std::string("Failed to read embedding values from seed file: '") + path + "'");
+        place_rows(vals.as<double>(), rows, c->n, c->ld, t->p, c->f64(), mode != KB2E_READ_VERBATIM,
+                   mode == KB2E_READ_SHRINK, c->stream);
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (table == 2) sync_wsnap(c);
+        // tables loaded from text alone (the evaluators) are complete once every table the model has is read
+        c->tables_read |= 1 << table;
+        if ((c->tables_read & 3) == 3 && (!c->w_elems || (c->tables_read & 4))) c->have_params = true;
         return KB2E_OK;
     });
 }

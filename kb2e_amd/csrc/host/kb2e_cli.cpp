@@ -186,30 +186,22 @@ void check(kb2e_ctx* ctx, kb2e_status st, const char* what) {
     }
 }
 
-bool readTable(const std::string& path, std::vector<double>& out, size_t count) {
-    FILE* f = fopen(path.c_str(), "r");
-    if (!f) return false;
-    out.resize(count);
-    for (size_t i = 0; i < count; ++i)
-        if (fscanf(f, "%lf", &out[i]) != 1) {
-            fclose(f);
-            return false;
-        }
-    fclose(f);
-    return true;
-}
-
-void writeTable(const std::string& path, const std::vector<double>& t, size_t rows, size_t cols) {
-    FILE* f = fopen(path.c_str(), "w");  // common/trainer.cpp:109-127
-    if (!f) {
+// common/trainer.cpp:109-127: "%.6lf\t" per value, "\n" per row, from the
+// device table (formatted on the device).
+void writeTable(kb2e_ctx* ctx, int table, const std::string& path) {
+    if (kb2e_write_table(ctx, table, path.c_str()) != KB2E_OK) {
         printf("Could not open output file: %s\n", path.c_str());
         exit(1);
     }
-    for (size_t i = 0; i < rows; ++i) {
-        for (size_t j = 0; j < cols; ++j) fprintf(f, "%.6lf\t", t[i * cols + j]);
-        fprintf(f, "\n");
+}
+
+// transr/trainer.cpp:90-113: the seed file into a device table (parsed on the
+// device), with the reference's message when it holds too few numbers.
+void readSeed(kb2e_ctx* ctx, int table, const std::string& path, int mode) {
+    if (kb2e_read_table(ctx, table, path.c_str(), mode) != KB2E_OK) {
+        printf("Failed to read embedding values from seed file: '%s'\n", path.c_str());
+        exit(1);
     }
-    fclose(f);
 }
 
 // ------------------------------------------------------------- trainer
@@ -244,10 +236,11 @@ class Trainer {  // the interface of common::Trainer (common/trainer.h:14-78)
         bfgs();
     }
 
+    // common/trainer.cpp:109-127: the device tables formatted on the device
     virtual void write() {
         const std::string m = method_name(args_.method);
-        writeTable(args_.outputDir + "/relation2vec." + m, rel_, numRelations_, args_.embeddingSize);
-        writeTable(args_.outputDir + "/entity2vec." + m, ent_, numEntities_, args_.embeddingSize);
+        writeTable(ctx_, 1, args_.outputDir + "/relation2vec." + m);
+        writeTable(ctx_, 0, args_.outputDir + "/entity2vec." + m);
     }
 
    protected:
@@ -256,7 +249,6 @@ class Trainer {  // the interface of common::Trainer (common/trainer.h:14-78)
     kb2e_ctx* ctx_ = nullptr;
     int numRelations_ = 0, numEntities_ = 0;
     std::vector<int> heads_, tails_, relations_;
-    std::vector<double> ent_, rel_, w_;
 
     // common/trainer.cpp:34-58: the initial tables, drawn from the same
     // glibc stream (seeded with --seed) inside the engine.
@@ -280,12 +272,10 @@ class Trainer {  // the interface of common::Trainer (common/trainer.h:14-78)
         check(nullptr, kb2e_create(&cfg, &ctx_), "create");
         check(ctx_, kb2e_upload_triples(ctx_, heads_.data(), tails_.data(), relations_.data(), (int64_t)heads_.size()),
               "upload_triples");
-        const size_t n = (size_t)args_.embeddingSize;
-        ent_.assign((size_t)numEntities_ * n, 0.0);
-        rel_.assign((size_t)numRelations_ * n, 0.0);
-        w_.assign(model_ == KB2E_TRANSH ? (size_t)numRelations_ * n
-                                        : model_ == KB2E_TRANSR ? (size_t)numRelations_ * n * n : 1, 0.0);
-        check(ctx_, kb2e_init_params(ctx_, ent_.data(), rel_.data(), w_.data()), "init_params");
+        // the reference's randn draws and row norms, made on the device from the
+        // same stream (kb2e_init_params is the host form of the same thing)
+        int64_t ties = 0;
+        check(ctx_, kb2e_init_params_device(ctx_, nullptr, nullptr, nullptr, &ties), "init_params");
     }
 
     // common/trainer.cpp:69-107, on the GPU.
@@ -297,7 +287,6 @@ class Trainer {  // the interface of common::Trainer (common/trainer.h:14-78)
             printf("Epoch: %d, Loss: %f\n", epoch, loss);
             fflush(stdout);
         }
-        check(ctx_, kb2e_download_params(ctx_, ent_.data(), rel_.data(), w_.data()), "download_params");
     }
 };
 
@@ -306,8 +295,7 @@ class TransHTrainer : public Trainer {  // transh/trainer.cpp:94-105
     using Trainer::Trainer;
     void write() override {
         Trainer::write();
-        writeTable(args_.outputDir + "/weights." + method_name(args_.method), w_, numRelations_,
-                   args_.embeddingSize);
+        writeTable(ctx_, 2, args_.outputDir + "/weights." + method_name(args_.method));
     }
 };
 
@@ -316,26 +304,17 @@ class TransRTrainer : public Trainer {
     using Trainer::Trainer;
     void write() override {  // transr/trainer.cpp:128-142
         Trainer::write();
-        writeTable(args_.outputDir + "/weights." + method_name(args_.method), w_,
-                   (size_t)numRelations_ * args_.embeddingSize, args_.embeddingSize);
+        writeTable(ctx_, 2, args_.outputDir + "/weights." + method_name(args_.method));
     }
 
    protected:
     void prepTrain() override {  // transr/trainer.cpp:70-114
         Trainer::prepTrain();
-        const size_t n = (size_t)args_.embeddingSize;
-        std::vector<double> E, R;
+        // seed files parsed on the device; entities unit-normed, relations verbatim
         std::string path = args_.seedDataDir + "/entity2vec." + method_name(args_.seedMethod);
-        if (!readTable(path, E, (size_t)numEntities_ * n)) {
-            printf("Failed to read embedding values from seed file: '%s'\n", path.c_str());
-            exit(1);
-        }
+        readSeed(ctx_, 0, path, KB2E_READ_UNIT);
         path = args_.seedDataDir + "/relation2vec." + method_name(args_.seedMethod);
-        if (!readTable(path, R, (size_t)numRelations_ * n)) {
-            printf("Failed to read embedding values from seed file: '%s'\n", path.c_str());
-            exit(1);
-        }
-        check(ctx_, kb2e_transr_seed(ctx_, E.data(), R.data()), "transr_seed");
+        readSeed(ctx_, 1, path, KB2E_READ_VERBATIM);
     }
 };
 
@@ -392,26 +371,6 @@ int eval_main(int argc, char** argv, kb2e_model model) {
         printf("Could not find weight embedding file: %s. Make sure to specify the path and/or train.\n", wPath.c_str());
         exit(2);
     }
-    std::vector<double> R, E, W;
-    if (!readTable(relPath, R, (size_t)nr * n)) {
-        printf("Failed to read embedding values from file: '%s'\n", relPath.c_str());
-        exit(1);
-    }
-    if (!readTable(entPath, E, (size_t)ne * n)) {
-        printf("Failed to read embedding values from file: '%s'\n", entPath.c_str());
-        exit(1);
-    }
-    for (int i = 0; i < ne; i++) {  // common/evaluation.cpp:99-102
-        const double len = vec_len(&E[(size_t)i * n], n);
-        if (len - 1 > 1e-3) std::cout << "wrong_entity" << i << ' ' << len << std::endl;
-    }
-    if (model != KB2E_TRANSE) {
-        const size_t cnt = model == KB2E_TRANSH ? (size_t)nr * n : (size_t)nr * n * n;
-        if (!readTable(wPath, W, cnt)) {
-            printf("Failed to read embedding weight values from seed file: '%s'\n", wPath.c_str());
-            exit(1);
-        }
-    }
     kb2e_config cfg;
     kb2e_default_config(&cfg);
     cfg.model = model;
@@ -424,7 +383,27 @@ int eval_main(int argc, char** argv, kb2e_model model) {
     cfg.device = args.device;
     kb2e_ctx* ctx = nullptr;
     check(nullptr, kb2e_create(&cfg, &ctx), "create");
-    check(ctx, kb2e_upload_params(ctx, E.data(), R.data(), W.empty() ? nullptr : W.data()), "upload_params");
+    // the embedding files parsed on the device (EmbeddingEvaluation::loadEmbeddings)
+    if (kb2e_read_table(ctx, 1, relPath.c_str(), KB2E_READ_VERBATIM) != KB2E_OK) {
+        printf("Failed to read embedding values from file: '%s'\n", relPath.c_str());
+        exit(1);
+    }
+    if (kb2e_read_table(ctx, 0, entPath.c_str(), KB2E_READ_VERBATIM) != KB2E_OK) {
+        printf("Failed to read embedding values from file: '%s'\n", entPath.c_str());
+        exit(1);
+    }
+    {
+        std::vector<double> E((size_t)ne * n);
+        check(ctx, kb2e_download_params(ctx, E.data(), nullptr, nullptr), "download_params");
+        for (int i = 0; i < ne; i++) {  // common/evaluation.cpp:99-102
+            const double len = vec_len(&E[(size_t)i * n], n);
+            if (len - 1 > 1e-3) std::cout << "wrong_entity" << i << ' ' << len << std::endl;
+        }
+    }
+    if (model != KB2E_TRANSE && kb2e_read_table(ctx, 2, wPath.c_str(), KB2E_READ_VERBATIM) != KB2E_OK) {
+        printf("Failed to read embedding weight values from seed file: '%s'\n", wPath.c_str());
+        exit(1);
+    }
     double out[5];
     if (model == KB2E_TRANSR && args.transrCompat) {
         // the reference's evalTransR: energy work vectors accumulate over the

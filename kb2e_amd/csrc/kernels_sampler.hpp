@@ -18,6 +18,7 @@
 #pragma once
 
 #include "kernels_common.hpp"
+#include "kernels_glibc.hpp"
 
 namespace kb2e {
 
@@ -135,66 +136,6 @@ __global__ __launch_bounds__(256) void sample_chain_kernel(ChainArgs a) {
     a.side[s] = ok ? a.sidefin[p] : 0;
     // Chain positions increase, so the last sample is valid iff all are.
     if (s == a.nsamples - 1) *a.consumed = ok ? (int64_t)a.next[p] : -1;
-}
-
-// ---- the epoch's raw glibc words, made on the device -----------------------
-//
-// glibc_starts: one wave walks the epoch in blocks of L words: the window
-//   before block p+1 is rows L-31..L-1 of the jump table applied to the window
-//   before block p (31 x 31 multiply-adds mod 2^32 per block).
-// glibc_words: word i = pL + t is sum_m C[m][t] * start_p[m], independently.
-// raw[0..31) = the starting window, raw[31 + i] = word i (raw), words[i] =
-// raw >> 1 (what rand() returns).
-struct GlibcWindow {
-    uint32_t w[31];
-};
-
-__global__ __launch_bounds__(64) void glibc_starts_kernel(GlibcWindow win, const uint32_t* C, int32_t L,
-                                                          int32_t nblocks, uint32_t* starts, uint32_t* raw) {
-    __shared__ uint32_t cur[32];
-    __shared__ uint32_t tail[31][32];  // tail[j][m] = C[m][L - 31 + j]
-    const int l = threadIdx.x;
-    for (int q = l; q < 31 * 31; q += 64) {
-        const int j = q / 31, m = q % 31;
-        tail[j][m] = C[(size_t)m * L + (L - 31 + j)];
-    }
-    if (l < 31) {
-        cur[l] = win.w[l];
-        raw[l] = win.w[l];
-    }
-    __syncthreads();
-    for (int p = 0; p < nblocks; ++p) {
-        uint32_t v = 0;
-        if (l < 31) {
-            starts[(size_t)p * 31 + l] = cur[l];
-#pragma unroll
-            for (int m = 0; m < 31; ++m) v += tail[l][m] * cur[m];
-        }
-        __syncthreads();
-        if (l < 31) cur[l] = v;
-        __syncthreads();
-    }
-}
-
-__global__ __launch_bounds__(256) void glibc_words_kernel(const uint32_t* C, int32_t L, const uint32_t* starts,
-                                                          int64_t nraw, uint32_t* raw, int32_t* words) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nraw) return;
-    const int64_t p = i / L;
-    const int t = (int)(i - p * L);
-    const uint32_t* st = starts + p * 31;
-    uint32_t v = 0;
-#pragma unroll
-    for (int m = 0; m < 31; ++m) v += C[(size_t)m * L + t] * st[m];
-    raw[31 + i] = v;
-    words[i] = (int32_t)(v >> 1);
-}
-
-// The generator window after the epoch's `consumed` words: raw[used .. used + 31).
-__global__ void glibc_window_kernel(const uint32_t* raw, const int64_t* consumed, uint32_t* out) {
-    const int l = threadIdx.x;
-    const int64_t used = *consumed;
-    if (l < 31) out[l] = used >= 0 ? raw[used + l] : 0u;
 }
 
 }  // namespace kb2e

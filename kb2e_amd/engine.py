@@ -26,8 +26,10 @@ EXPORTS = [
     "kb2e_set_transr_work", "kb2e_set_sample_stream", "kb2e_get_sample_stream", "kb2e_train_epoch", "kb2e_train_batches",
     "kb2e_synchronize", "kb2e_take_stats", "kb2e_rng_next", "kb2e_profile_enable", "kb2e_profile_query",
     "kb2e_device_bytes", "kb2e_device_tables", "kb2e_renormalize", "kb2e_evaluate", "kb2e_evaluate_transr_compat",
-    "kb2e_renormalize_rows",
+    "kb2e_renormalize_rows", "kb2e_init_params_device", "kb2e_write_table", "kb2e_format_table",
+    "kb2e_read_table",
 ]
+READ_VERBATIM, READ_UNIT, READ_SHRINK = 0, 1, 2
 
 
 class Config(C.Structure):
@@ -57,6 +59,10 @@ def lib():
             "kb2e_last_error": (C.c_char_p, [vp]),
             "kb2e_upload_triples": (i32, [vp, i32p, i32p, i32p, i64]),
             "kb2e_init_params": (i32, [vp, dp, dp, dp]),
+            "kb2e_init_params_device": (i32, [vp, dp, dp, dp, C.POINTER(i64)]),
+            "kb2e_write_table": (i32, [vp, i32, C.c_char_p]),
+            "kb2e_format_table": (i32, [vp, i32, C.c_char_p, i64, C.POINTER(i64)]),
+            "kb2e_read_table": (i32, [vp, i32, C.c_char_p, i32]),
             "kb2e_upload_params": (i32, [vp, dp, dp, dp]),
             "kb2e_transr_seed": (i32, [vp, dp, dp]),
             "kb2e_download_params": (i32, [vp, dp, dp, dp]),
@@ -149,6 +155,35 @@ class Engine:
         w = np.zeros(self.wshape()) if self.wshape() else None
         self._check(lib().kb2e_init_params(self.h, _dp(ent), _dp(rel), _dp(w)), "init_params")
         return ent, rel, w
+
+    def init_params_device(self, fetch=True):
+        """Trainer::prepTrain's draws made on the device (same values, same rng
+        position); returns (ent, rel, w, near_ties), the tables None if not fetched."""
+        ties = C.c_int64(0)
+        if not fetch:
+            self._check(lib().kb2e_init_params_device(self.h, None, None, None, C.byref(ties)), "init_params_device")
+            return None, None, None, ties.value
+        ent = np.zeros((self.ne, self.n))
+        rel = np.zeros((self.nr, self.n))
+        w = np.zeros(self.wshape()) if self.wshape() else None
+        self._check(lib().kb2e_init_params_device(self.h, _dp(ent), _dp(rel), _dp(w), C.byref(ties)),
+                    "init_params_device")
+        return ent, rel, w, ties.value
+
+    def write_table(self, table, path):
+        """The device table (0 entities, 1 relations, 2 weights) as the reference's "%.6lf\\t" text file."""
+        self._check(lib().kb2e_write_table(self.h, int(table), os.fsencode(path)), "write_table")
+
+    def format_table(self, table):
+        need = C.c_int64(0)
+        lib().kb2e_format_table(self.h, int(table), None, 0, C.byref(need))
+        buf = C.create_string_buffer(max(1, need.value))
+        self._check(lib().kb2e_format_table(self.h, int(table), buf, need.value, C.byref(need)), "format_table")
+        return buf.raw[:need.value]
+
+    def read_table(self, table, path, mode=READ_VERBATIM):
+        """Load a device table from "%lf" text (parsed on the device); mode: READ_VERBATIM / READ_UNIT / READ_SHRINK."""
+        self._check(lib().kb2e_read_table(self.h, int(table), os.fsencode(path), int(mode)), "read_table")
 
     def transr_seed(self, ent, rel):
         ent = np.ascontiguousarray(ent, dtype=np.float64)

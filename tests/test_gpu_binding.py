@@ -74,12 +74,8 @@ def test_binding_transr_fixed(tmp_path):
 def test_binding_fails_loudly_without_engine(tmp_path):
     """CPU box: the reference's parse/load/init run, then kb2e_create reports
     the missing GPU the reference's way (message + exit(1))."""
-    try:
-        import torch
-        if torch.cuda.is_available():
-            pytest.skip("a GPU is present")
-    except ImportError:
-        pass
+    if os.path.exists("/dev/kfd"):  # a GPU box: the engine would start
+        pytest.skip("GPU present")
     res, out = _run(tmp_path, "trainTransE", "transe_l1_bern", check=False)
     assert res.returncode == 1, res.stdout
     assert "kb2e_create failed" in res.stdout and "Number of Entities: 200" in res.stdout
