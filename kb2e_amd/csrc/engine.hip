@@ -38,6 +38,7 @@
 #include "kernels_parallel.hpp"
 #include "kernels_transr_parallel.hpp"
 #include "kernels_transr_mfma.hpp"
+#include "transr_cons.hpp"
 #include "kernels_transh_parallel.hpp"
 #include "textio.hpp"
 
@@ -143,6 +144,8 @@ struct kb2e_ctx {
     int32_t rpar_St = 8, rpar_max_tiles = 1, rpar_tile_threads = 256;
     bool rpar_no_constraint = false;
     bool rpar_mfma = false;  // matrix-core tile kernels (kernels_transr_mfma.hpp)
+    bool rpar_cons_wave = false;  // transRNorm rounds in one wave's registers (kernels_transr_cons.hpp)
+    size_t rpar_cons_lds = 0;
     DevBuf rpar_pflag, rpar_cons_tile;
     DevBuf rpar_y, rpar_wpart, rpar_rpart, rpar_tile_act, rpar_pair, rpar_relpair, rpar_relpair_stamp, rpar_tiles,
         rpar_ntiles, rpar_tile_first, rpar_rel_begin, rpar_scan;
@@ -1458,12 +1461,18 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
         if (getenv("KB2E_RPAR_STATS")) {  // transRNorm rounds of the PARALLEL TransR schedule
             unsigned long long st[16];
             HIPCHK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_rpar_rounds), sizeof(st)));
+            cons_wave_take_stats(st);  // the register-resident kernel's own counters
             fprintf(stderr, "rpar_rounds rounds of row blocks %llu, tiles with violators %llu, most rounds of a block %llu\n",
                     st[0], st[1], st[2]);
             fprintf(stderr, "rpar_cons cycles: setup %llu, P0+rounds %llu, records %llu, longest block %llu, blocks %llu\n",
                     st[3], st[4], st[5], st[6], st[7]);
-            fprintf(stderr, "rpar_rounds wave 0: loads+mfma issue %llu, barriers %llu, update part %llu, lockstep rounds %llu, "
-                    "tail %llu, G+ballot %llu\n", st[8], st[9], st[10], st[11], st[12], st[13]);
+            if (c->rpar_cons_wave)
+                fprintf(stderr, "rpar_cons wave kernel: longest setup %llu, P0+rounds %llu, records %llu, a wave's "
+                        "rounds %llu; MFMA rounds before the VALU tail %llu, blocks entering it %llu\n",
+                        st[8], st[9], st[10], st[11], st[12], st[13]);
+            else
+                fprintf(stderr, "rpar_rounds wave 0: loads+mfma issue %llu, barriers %llu, update part %llu, lockstep "
+                        "rounds %llu, tail %llu, G+ballot %llu\n", st[8], st[9], st[10], st[11], st[12], st[13]);
             std::memset(st, 0, sizeof(st));
             HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_rpar_rounds), st, sizeof(st)));
         }

@@ -349,7 +349,7 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
 //   (MFMA), a flag per update slot (bf.pflag: the record is valid) and the
 //   tile's violator count (bf.cons_tile: 0 = no partial).
 // transRNorm statistics (tools): rounds summed over row blocks, tiles with violators, most rounds of a block
-__device__ unsigned long long g_rpar_rounds[16];
+static __device__ unsigned long long g_rpar_rounds[16];
 
 // kConsNB: the column blocks of 16, exactly (NP = 16 kConsNB): every loop over
 // them and over the k-steps below NP has a compile-time trip count.

@@ -79,8 +79,10 @@ struct RParBufs {
     uint32_t stamp;
     // matrix-core transRNorm (kernels_transr_mfma.hpp); null on the VALU path
     uint8_t* pflag;      // [B][2][2] the pair record of the slot is valid this batch
-    int32_t* cons_tile;  // [tiles] row blocks with violators per tile (0: no matrix partial)
+    int32_t* cons_tile;  // [tiles][cons_ppt] the transRNorm matrix partial is valid (0: none)
+    int32_t cons_ppt;    // transRNorm matrix partials per tile (1, or one per row block)
     int32_t stats;       // count transRNorm rounds (tools)
+    int32_t dbg;         // transRNorm wave kernel: phases skipped for timing experiments (tools; wrong results)
 };
 
 __host__ __device__ constexpr int rm_up16_host_dev(int v) { return (v + 15) & ~15; }
@@ -340,33 +342,37 @@ __global__ __launch_bounds__(256) void transr_rel_rows_kernel(RParArgs a, RParBu
     const int n = a.n, ld = a.ld;
     const int tb = a.tile_first[a.batch_seg[a.batch]];  // partials are indexed by tile within the batch
     // GRAD step: the reference touches (and normalises) a relation only through
-    // an active update; matrix-core transRNorm step: only tiles whose pairs moved
-    // have a partial
+    // an active update; matrix-core transRNorm step: only the partials whose
+    // pairs moved (cons_ppt per tile, in (tile, row block) order)
     const bool sel = !NORM && bf.cons_tile;
-    // the tiles that carry a partial, 64 flags per load (lane-parallel, not a
+    // partial slots u in [u0, u1): tiles (GRAD, VALU transRNorm) or (tile, block) pairs
+    const int ppt = sel ? bf.cons_ppt : 1;
+    const int u0 = sel ? (t0 - tb) * ppt : t0, u1 = sel ? (t1 - tb) * ppt : t1;
+    const int ub = sel ? 0 : tb;  // slot u's partial is number u - ub of the batch
+    // the slots that carry a partial, 64 flags per load (lane-parallel, not a
     // serial scan: a hot relation has tens of tiles)
     auto flags = [&](int base) {
-        const int t = base + lane_id();
-        const int f = t < t1 ? (sel ? bf.cons_tile[t - tb] : a.tile_act[t]) : 0;
+        const int u = base + lane_id();
+        const int f = u < u1 ? (sel ? bf.cons_tile[u] : a.tile_act[u]) : 0;
         return (uint64_t)__ballot(f != 0);
     };
     uint64_t any = 0;
-    for (int base = t0; base < t1 && !any; base += kWave) any = flags(base);
+    for (int base = u0; base < u1 && !any; base += kWave) any = flags(base);
     if (!any) return;
     T* row = j < n ? bf.W + ((int64_t)r * n + j) * ld : bf.rel + (int64_t)r * ld;
     T v[2];
     lane_pair_load(row, n, v);
-    for (int base = t0; base < t1; base += kWave) {
+    for (int base = u0; base < u1; base += kWave) {
         // every tile's partial (the VALU transRNorm step writes one for each
         // tile), or only the flagged ones of the matrix-core transRNorm step
-        uint64_t m = sel ? flags(base) : (uint64_t)__ballot(base + lane_id() < t1);
-        while (m) {  // eight partial rows in flight, summed in tile order
+        uint64_t m = sel ? flags(base) : (uint64_t)__ballot(base + lane_id() < u1);
+        while (m) {  // eight partial rows in flight, summed in slot order
             T p[8][2];
             bool use[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 use[q] = m != 0;
-                const int64_t lt = use[q] ? base + __builtin_ctzll(m) - tb : 0;
+                const int64_t lt = use[q] ? base + __builtin_ctzll(m) - ub : 0;
                 m &= m - 1;
                 if (use[q]) lane_pair_load(j < n ? bf.wpart + (lt * n + j) * ld : bf.rpart + lt * ld, n, p[q]);
             }
@@ -680,7 +686,7 @@ __global__ __launch_bounds__(1024) void transr_entity_kernel(RParArgs a, RParBuf
 // energies), one thread per (head/tail, element), coalesced rows.
 constexpr int kScanChunk = 64;
 
-__global__ __launch_bounds__(256) void rpar_scan_sums_kernel(const double* proj, int64_t calls, int32_t ld,
+static __attribute__((unused)) __global__ __launch_bounds__(256) void rpar_scan_sums_kernel(const double* proj, int64_t calls, int32_t ld,
                                                              int32_t n, double* sums) {
     const int c = blockIdx.x;
     const int64_t c0 = (int64_t)c * kScanChunk, c1 = min<int64_t>(calls, c0 + kScanChunk);
@@ -769,7 +775,7 @@ __global__ __launch_bounds__(256) void rpar_scan_energy_kernel(RParArgs a, RParB
 
 // Tiles per segment (relation segments: ceil(samples / St); entity segments 0),
 // and the first relation segment of every batch.
-__global__ __launch_bounds__(256) void rtile_count_kernel(const uint64_t* keys, const int32_t* seg_start,
+static __attribute__((unused)) __global__ __launch_bounds__(256) void rtile_count_kernel(const uint64_t* keys, const int32_t* seg_start,
                                                           const int32_t* nseg_p, int64_t cap, KeyLayout kl,
                                                           int32_t ne, int32_t St, int32_t* ntiles,
                                                           int32_t* rel_begin) {
@@ -792,7 +798,7 @@ __global__ __launch_bounds__(256) void rtile_count_kernel(const uint64_t* keys, 
     }
 }
 
-__global__ __launch_bounds__(256) void rtile_scatter_kernel(const int32_t* ntiles, const int32_t* tile_first,
+static __attribute__((unused)) __global__ __launch_bounds__(256) void rtile_scatter_kernel(const int32_t* ntiles, const int32_t* tile_first,
                                                             const int32_t* nseg_p, RTile* tiles) {
     const int nseg = *nseg_p;
     for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x)

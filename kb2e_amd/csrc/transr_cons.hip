@@ -1,0 +1,65 @@
+// transr_cons.hip -- the register-resident transRNorm kernel of the PARALLEL
+// TransR schedule (kernels_transr_cons.hpp), instantiated for every live
+// k-step count 1..16 (n <= 64) in FP64 and FP32.
+#include "transr_cons.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <utility>
+
+#include "hip_util.hpp"
+#include "kernels_transr_cons.hpp"
+
+namespace kb2e {
+
+namespace {
+
+template <typename T, int KS>
+const void* fn_at() {
+    return (const void*)transr_cons_wave_kernel<T, KS>;
+}
+
+template <typename T, int... KS>
+const void* fn_table(int ks, std::integer_sequence<int, KS...>) {
+    const void* tab[] = {fn_at<T, KS + 1>()...};
+    return tab[ks - 1];
+}
+
+template <typename T>
+const void* cons_fn(int n) {
+    if (!cons_wave_supported(n)) throw std::runtime_error("transRNorm wave kernel: n > 64");
+    return fn_table<T>(cons_live_steps<T>(n), std::make_integer_sequence<int, 16>{});
+}
+
+}  // namespace
+
+bool cons_wave_supported(int n) { return n >= 1 && n <= 64; }
+
+size_t cons_wave_setup(int n, int St, int esize) {
+    const size_t lds = esize == 8 ? rcons_lds<double>(n, St) : rcons_lds<float>(n, St);
+    HIPCHK(hipFuncSetAttribute(esize == 8 ? cons_fn<double>(n) : cons_fn<float>(n),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    return lds;
+}
+
+template <typename T>
+void cons_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, size_t lds, hipStream_t stream) {
+    RParArgs aa = a;
+    RParBufs<T> bb = bf;
+    void* args[] = {&aa, &bb};
+    HIPCHK(hipLaunchKernel(cons_fn<T>(a.n), dim3(grid), dim3(kConsWaves * kWave), args, lds, stream));
+}
+
+template void cons_wave_launch<double>(const RParArgs&, const RParBufs<double>&, int, size_t, hipStream_t);
+template void cons_wave_launch<float>(const RParArgs&, const RParBufs<float>&, int, size_t, hipStream_t);
+
+void cons_wave_take_stats(unsigned long long (&st)[16]) {
+    unsigned long long mine[16];
+    HIPCHK(hipMemcpyFromSymbol(mine, HIP_SYMBOL(g_cons_stats), sizeof(mine)));
+    for (int k = 0; k < 16; ++k) st[k] = (k == 2 || k == 6) ? std::max(st[k], mine[k]) : st[k] + mine[k];
+    std::memset(mine, 0, sizeof(mine));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_cons_stats), mine, sizeof(mine)));
+}
+
+}  // namespace kb2e

@@ -1,0 +1,24 @@
+// transr_cons.hpp -- host entry points of the register-resident transRNorm
+// kernel (kernels_transr_cons.hpp), compiled in its own translation unit
+// (transr_cons.hip): one instantiation per live k-step count.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "kernels_transr_parallel.hpp"
+
+namespace kb2e {
+
+constexpr int kConsPpt = 1;  // transRNorm matrix partials per tile (transr_rel_rows_kernel cons_ppt)
+
+// Does the kernel cover this width (n <= 64)?
+bool cons_wave_supported(int n);
+// Dynamic LDS bytes of one workgroup; raises the kernels' LDS limit to it.
+size_t cons_wave_setup(int n, int St, int esize);
+// One workgroup (four waves) per tile of the batch.
+template <typename T>
+void cons_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, size_t lds, hipStream_t stream);
+// Adds the kernel's round statistics (g_rpar_rounds layout) to st and resets them.
+void cons_wave_take_stats(unsigned long long (&st)[16]);
+
+}  // namespace kb2e

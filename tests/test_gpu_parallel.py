@@ -122,8 +122,16 @@ def test_transr_parallel_fixed(dim, distance, St, mfma, monkeypatch):
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, distance=distance, mfma=mfma)
 
 
+@pytest.mark.parametrize("dim,distance,St,compat", [(20, 0, 8, False), (50, 0, 8, True), (33, 1, 4, False)])
+def test_transr_parallel_cons_tile_kernel(dim, distance, St, compat, monkeypatch):
+    """The LDS-round transRNorm kernel (transr_cons_tile_kernel), which n <= 64
+    replaces by the register-resident one (kernels_transr_cons.hpp) by default."""
+    monkeypatch.setenv("KB2E_RPAR_CONS", "tile")
+    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, distance=distance, compat=compat)
+
+
 @pytest.mark.parametrize("mfma", [True, False])
-@pytest.mark.parametrize("dim,St", [(20, 8), (65, 2), (100, 8)])
+@pytest.mark.parametrize("dim,St", [(20, 8), (50, 8), (65, 2), (100, 8)])
 def test_transr_parallel_compat(dim, St, mfma, monkeypatch):
     """The reference's accumulating work-vector energy (transr/transr.cpp:20-25).
     n = 65: matrix-core images at St = 2; n = 100 (K5): the VALU tile kernels
