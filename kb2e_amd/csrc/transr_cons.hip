@@ -10,26 +10,36 @@
 
 #include "hip_util.hpp"
 #include "kernels_transr_cons.hpp"
+#include "kernels_transr_wave.hpp"
 
 namespace kb2e {
 
 namespace {
 
+enum Kind { kCons, kGrad, kProj };
+
 template <typename T, int KS>
-const void* fn_at() {
-    return (const void*)transr_cons_wave_kernel<T, KS>;
+const void* fn_at(Kind k) {
+    return k == kCons ? (const void*)transr_cons_wave_kernel<T, KS>
+           : k == kGrad ? (const void*)transr_grad_wave_kernel<T, KS>
+                        : (const void*)transr_proj_wave_kernel<T, KS>;
 }
 
 template <typename T, int... KS>
-const void* fn_table(int ks, std::integer_sequence<int, KS...>) {
-    const void* tab[] = {fn_at<T, KS + 1>()...};
+const void* fn_table(Kind k, int ks, std::integer_sequence<int, KS...>) {
+    const void* tab[] = {fn_at<T, KS + 1>(k)...};
     return tab[ks - 1];
 }
 
 template <typename T>
+const void* kernel_fn(Kind k, int n) {
+    if (!cons_wave_supported(n)) throw std::runtime_error("TransR wave kernels: n > 64");
+    return fn_table<T>(k, cons_live_steps<T>(n), std::make_integer_sequence<int, 16>{});
+}
+
+template <typename T>
 const void* cons_fn(int n) {
-    if (!cons_wave_supported(n)) throw std::runtime_error("transRNorm wave kernel: n > 64");
-    return fn_table<T>(cons_live_steps<T>(n), std::make_integer_sequence<int, 16>{});
+    return kernel_fn<T>(kCons, n);
 }
 
 }  // namespace
@@ -50,6 +60,29 @@ void cons_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, size_t
     void* args[] = {&aa, &bb};
     HIPCHK(hipLaunchKernel(cons_fn<T>(a.n), dim3(grid), dim3(kConsWaves * kWave), args, lds, stream));
 }
+
+template <typename T>
+void grad_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, hipStream_t stream) {
+    RParArgs aa = a;
+    RParBufs<T> bb = bf;
+    void* args[] = {&aa, &bb};
+    HIPCHK(hipLaunchKernel(kernel_fn<T>(kGrad, a.n), dim3(grid), dim3(kConsWaves * kWave), args, 0, stream));
+}
+
+template <typename T>
+void proj_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, hipStream_t stream) {
+    RParArgs aa = a;
+    RParBufs<T> bb = bf;
+    void* args[] = {&aa, &bb};
+    const size_t lds = sizeof(T) * (size_t)rm_np(a.n) * rm_ld(a.n);
+    HIPCHK(hipLaunchKernel(kernel_fn<T>(kProj, a.n), dim3(grid), dim3(kProjWaves * kWave), args, lds, stream));
+}
+
+template void proj_wave_launch<double>(const RParArgs&, const RParBufs<double>&, int, hipStream_t);
+template void proj_wave_launch<float>(const RParArgs&, const RParBufs<float>&, int, hipStream_t);
+
+template void grad_wave_launch<double>(const RParArgs&, const RParBufs<double>&, int, hipStream_t);
+template void grad_wave_launch<float>(const RParArgs&, const RParBufs<float>&, int, hipStream_t);
 
 template void cons_wave_launch<double>(const RParArgs&, const RParBufs<double>&, int, size_t, hipStream_t);
 template void cons_wave_launch<float>(const RParArgs&, const RParBufs<float>&, int, size_t, hipStream_t);

@@ -18,6 +18,14 @@ size_t cons_wave_setup(int n, int St, int esize);
 // One workgroup (four waves) per tile of the batch.
 template <typename T>
 void cons_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, size_t lds, hipStream_t stream);
+// Phase A of the batch's tiles (projections, x, d, y; energies + hinge, or the compat
+// projections for the work-vector scan), one two-wave workgroup per tile (kernels_transr_wave.hpp).
+template <typename T>
+void proj_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, hipStream_t stream);
+// The tile gradient partials dW, dr (+ tile_act) of the batch, one workgroup per tile
+// (kernels_transr_wave.hpp); needs bf.x, bf.d and the hinge decisions in place.
+template <typename T>
+void grad_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, hipStream_t stream);
 // Adds the kernel's round statistics (g_rpar_rounds layout) to st and resets them.
 void cons_wave_take_stats(unsigned long long (&st)[16]);
 
