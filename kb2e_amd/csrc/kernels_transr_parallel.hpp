@@ -330,8 +330,7 @@ __global__ __launch_bounds__(256) void transr_tile_kernel(RParArgs a, RParBufs<T
 // then the unit norm (common::norm(v, false), transr/trainer.cpp:174-180) when
 // NORM.  Without NORM (the transRNorm step) only the matrix rows change.
 template <typename T, bool NORM>
-__global__ __launch_bounds__(256) void transr_rel_rows_kernel(RParArgs a, RParBufs<T> bf) {
-    const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+__device__ __forceinline__ void transr_rel_rows_wave(RParArgs a, RParBufs<T> bf, int gw) {  // by value: no scratch copy
     const int rows = a.n + 1;
     const int s = a.rel_begin[a.batch] + gw / rows;
     const int j = gw % rows;
@@ -351,9 +350,11 @@ __global__ __launch_bounds__(256) void transr_rel_rows_kernel(RParArgs a, RParBu
     const int ub = sel ? 0 : tb;  // slot u's partial is number u - ub of the batch
     // the slots that carry a partial, 64 flags per load (lane-parallel, not a
     // serial scan: a hot relation has tens of tiles)
-    auto flags = [&](int base) {
+    // (captures by value: a reference to the argument structs would put them in scratch)
+    const int32_t* const fl = sel ? bf.cons_tile : a.tile_act;
+    auto flags = [fl, u1](int base) {
         const int u = base + lane_id();
-        const int f = u < u1 ? (sel ? bf.cons_tile[u] : a.tile_act[u]) : 0;
+        const int f = u < u1 ? fl[u] : 0;
         return (uint64_t)__ballot(f != 0);
     };
     uint64_t any = 0;
@@ -390,6 +391,11 @@ __global__ __launch_bounds__(256) void transr_rel_rows_kernel(RParArgs a, RParBu
         v[1] = v[1] / len;
     }
     lane_pair_store(row, n, v);
+}
+
+template <typename T, bool NORM>
+__global__ __launch_bounds__(256) void transr_rel_rows_kernel(RParArgs a, RParBufs<T> bf) {
+    transr_rel_rows_wave<T, NORM>(a, bf, (blockIdx.x * blockDim.x + threadIdx.x) >> 6);
 }
 
 // transRNorm (transr/trainer.cpp:35-64) per tile, on W'_r and the entity rows
@@ -621,18 +627,19 @@ __device__ __forceinline__ void rpar_entity_finish(const RParArgs& a, const RPar
     lane_pair_store(ptr, n, v);
 }
 
+// the entity rows of workgroup `bid` of G (1024 threads)
 template <typename T, bool GRAD>
-__global__ __launch_bounds__(1024) void transr_entity_kernel(RParArgs a, RParBufs<T> bf, int32_t long_min) {
+__device__ __forceinline__ void transr_entity_block(RParArgs a, RParBufs<T> bf, int32_t long_min, int bid, int G) {
     __shared__ T part[kRParWaves][2][kWave];
     __shared__ int flags[2];
     __shared__ int longs[1024], nlong;
     const int w = threadIdx.x >> 6, l = lane_id();
     const int s0 = a.batch_seg[a.batch], s1 = a.rel_begin[a.batch];  // entity segments sort first
-    const int G = gridDim.x;
-    // long segments: whole workgroup, segments s0 + blockIdx.x, s0 + blockIdx.x + G, ... that are
+    const int blockIdx_x = bid;
+    // long segments: whole workgroup, segments s0 + blockIdx_x, s0 + blockIdx_x + G, ... that are
     // long, found by one thread each (blockDim.x candidates per pass; the order between
     // segments is immaterial, each is a different row)
-    for (int c0 = s0 + blockIdx.x; c0 < s1; c0 += G * (int)blockDim.x) {
+    for (int c0 = s0 + blockIdx_x; c0 < s1; c0 += G * (int)blockDim.x) {
         if (threadIdx.x == 0) nlong = 0;
         __syncthreads();
         const int cs = c0 + G * (int)threadIdx.x;
@@ -666,7 +673,7 @@ __global__ __launch_bounds__(1024) void transr_entity_kernel(RParArgs a, RParBuf
         }
     }
     // short segments: one wave each
-    for (int s = s0 + blockIdx.x * kRParWaves + w; s < s1; s += G * kRParWaves) {
+    for (int s = s0 + blockIdx_x * kRParWaves + w; s < s1; s += G * kRParWaves) {
         const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
         if (p1 - p0 >= long_min) continue;
         const int row = a.seg_row[s];
@@ -675,6 +682,20 @@ __global__ __launch_bounds__(1024) void transr_entity_kernel(RParArgs a, RParBuf
         rpar_entity_events<T, GRAD>(a, bf, row, p0, p1, 0, 1, acc, dirty, er);
         rpar_entity_finish<T, GRAD>(a, bf, row, acc, dirty, er);
     }
+}
+
+template <typename T, bool GRAD>
+__global__ __launch_bounds__(1024) void transr_entity_kernel(RParArgs a, RParBufs<T> bf, int32_t long_min) {
+    transr_entity_block<T, GRAD>(a, bf, long_min, blockIdx.x, gridDim.x);
+}
+
+// Both row passes of one step in one launch (they touch disjoint tables):
+// workgroups [0, egrid) the entity rows, the rest one wave per (relation, row).
+template <typename T, bool PASS1>
+__global__ __launch_bounds__(1024) void transr_rows_kernel(RParArgs a, RParBufs<T> bf, int32_t long_min,
+                                                           int32_t egrid) {
+    if ((int)blockIdx.x < egrid) transr_entity_block<T, PASS1>(a, bf, long_min, blockIdx.x, egrid);
+    else transr_rel_rows_wave<T, PASS1>(a, bf, (((int)blockIdx.x - egrid) * (int)blockDim.x + (int)threadIdx.x) >> 6);
 }
 
 // ---- compat energy: the work-vector prefix scan over the batch's calls -------

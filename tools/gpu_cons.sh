@@ -11,6 +11,7 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_parallel.py -x -v --timeout
 tail -2 $OUT/pytest.log
 timeout -k 10 200 python3 tools/probe_rounds.py compat 100 > $OUT/rounds.log 2>&1 || { echo "probe failed"; exit 1; }
 timeout -k 10 300 python3 bench.py --only --no-cpu-baseline --steps 100 --warmup 100 > $OUT/bench_wave.json 2> $OUT/bench_wave.err || { echo "bench failed"; exit 1; }
+KB2E_RPAR_FUSE=0 timeout -k 10 300 python3 bench.py --only --no-cpu-baseline --steps 100 --warmup 100 > $OUT/bench_nofuse.json 2> $OUT/bench_nofuse.err || { echo "bench nofuse failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
     python3 bench.py --only --no-cpu-baseline --no-epoch --steps 100 --warmup 100 > $OUT/trace.log 2>&1 || { echo "trace failed"; exit 1; }
 find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;

@@ -27,6 +27,8 @@ FAMILY = {"transe_fold_long_kernel": "fold_long", "transe_fold_kernel": "fold", 
 # kernel -> the bench.py phase it belongs to (the HIP-event spans of the engine)
 PHASE = [("transe_score", "score"), ("transh_score", "score"), ("transr_project", "score"),
          ("transr_compat", "score"), ("transr_tile", "score"), ("rpar_scan", "score"),
+         ("transr_proj_wave", "score"), ("transr_grad_wave", "score"), ("transr_rows", "apply"),
+         ("transr_cons", "apply"),
          ("transe_fold", "fold_phase"), ("transe_apply", "fold_phase|apply"), ("transh_w_apply", "fold_phase"),
          ("transh_orth", "fold_phase"), ("transr_rel_rows", "apply"), ("transr_entity", "apply"),
          ("transr_constraint", "apply"), ("owner_kernel", "relowner"), ("owner_reg_kernel", "relowner")]
@@ -123,6 +125,8 @@ def main(src, tag, config, prec, schedule="parallel", batches="200"):
              "(rocprofv3 --kernel-trace --stats; separate --pmc FETCH_SIZE / WRITE_SIZE passes).", "",
              "## bench.py line", "", "```", bench, "```", "", "## Kernel stats (rocprofv3 --stats)", "",
              "| kernel | calls | total ms | avg us | % |", "|---|---|---|---|---|"]
+    if config.startswith("transr"):  # not the TransE-init seed run of bench.py
+        stats = [r for r in stats if not r["Name"].startswith(("void kb2e::transe_", "kb2e::long_segments"))]
     for r in stats[:16]:
         lines.append(f"| {r['Name'][:60]} | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.2f} | "
                      f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} |")
