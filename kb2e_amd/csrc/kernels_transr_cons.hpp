@@ -82,13 +82,12 @@ __device__ __forceinline__ T row4_sum(T v) {
 constexpr int kConsWaves = 4;  // PP / 16 <= 4 row blocks (4 St + 1 <= 64)
 constexpr int kValuRows = 4;   // a block with this few moving rows iterates on the VALU
 
-// LDS (bytes): W0 [NP][NP + 2] | K [NP][NP + 2] | per wave SP [kValuRows][NP] |
-// int ent_of, slot_of, rowmap, posmap [PP], misc [8]  (76 KB at n = 50 in FP64:
-// two workgroups per CU)
+// LDS (bytes): W0 [NP][NP + 2] | K [NP][NP + 2] | per wave SP [kValuRows][NP] | int misc [8]
+// (75 KB at n = 50 in FP64: two workgroups per CU)
 template <typename T>
 __host__ __device__ constexpr size_t rcons_lds(int n, int St) {
     return sizeof(T) * (2 * (size_t)rm_np(n) * rm_ld(n) + (size_t)kConsWaves * kValuRows * rm_np(n)) +
-           sizeof(int) * (4 * (size_t)rm_up16(4 * St + 1) + 8);
+           sizeof(int) * 8 + 0 * (size_t)St;
 }
 
 // k-steps (of kmap) that hold a column below n: a prefix 0 .. KS - 1 of the
@@ -210,65 +209,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
     if (t >= a.tile_first[a.batch_seg[a.batch + 1]]) return;
     int r, e0, cnt;
     tile_range(a, t, r, e0, cnt);
+    (void)e0;
+    (void)cnt;
     const int n = a.n, ld = a.ld;
-    const int PP = rm_up16(4 * a.St + 1);
     const int w = threadIdx.x >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
     T* Wl = (T*)smem;
     T* KX = Wl + NP * L;
     T* SP = KX + NP * L + w * kValuRows * NP;  // this wave's VALU rounds: p rows
-    int* ent_of = (int*)(KX + NP * L + kConsWaves * kValuRows * NP);
-    int* slot_of = ent_of + PP;  // (kk * 2 + u) * 2 + role, -2 for (entity[r], r), -1 none
-    int* rowmap = slot_of + PP;  // compacted row -> pair
-    int* posmap = rowmap + PP;   // pair -> compacted row or -1
-    int* misc = posmap + PP;     // [0] rows, [1] the tile has a violator, [2 + b] row block b has one
-    const RTile tl = a.tiles[t];
+    int* misc = (int*)(KX + NP * L + kConsWaves * kValuRows * NP);  // [1] the tile has a violator, [2 + b] block b has one
     const unsigned long long ck0 = bf.stats ? clock64() : 0ull;
     const T lr = (T)a.lr;
+    // this wave's pair rows (compacted by transr_grad_wave_kernel) and their a0 rows as
+    // B fragments (not kept: the matrix partial re-reads them), loads issued before the barrier
+    const int nrows = bf.cnrows[blockIdx.x];
+    const int nblk = (nrows + 15) >> 4;
+    const bool mine = w < nblk;  // this wave owns pair rows [16 w, 16 w + 16)
+    const int32_t* cp = bf.cpairs + (int64_t)blockIdx.x * 2 * kCPairs;
+    const int row = w * 16 + l16;
+    const int e = row < nrows ? cp[row] : -1;
+    const int sl = row < nrows ? cp[kCPairs + row] : -1;
+    T af[KS];
+    {
+        const T* ar = bf.ent + (int64_t)(e < 0 ? 0 : e) * ld;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {  // unconditional loads (in-row index), masked by a
+            const int k = kmap<T>(s, kq);  // product: a select lets the compiler branch around each load
+            af[s] = ar[k < n ? k : 0] * ((e >= 0 && k < n) ? T(1) : T(0));
+        }
+    }
     if (w == 0) {
-        // (entity'[r], r) joins the relation's first tile if any of its tiles has an active update
-        bool relpair = false;
-        if (tl.q == 0 && r < a.ne) {
-            const int q0 = a.tile_first[tl.seg], q1 = a.tile_first[tl.seg + 1];
-            for (int q = q0; q < q1 && !relpair; q += kWave) relpair = __ballot(q + l < q1 && a.tile_act[q + l]) != 0;
-        }
-        const int npairs = 4 * cnt + (relpair ? 1 : 0);
-        // the pairs, then the first occurrence of each entity compacted in pair order
-        const int pq = l;
-        int ent = -1, slot = -1;
-        if (pq < 4 * cnt) {
-            const int q = pq >> 2, u = (pq >> 1) & 1, role = pq & 1;
-            const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
-            if (a.act[kk]) {
-                const int i0 = a.si[kk], jj = a.sj[kk];
-                const int h = a.heads[i0], tt = a.tails[i0];
-                const int hh = u ? (a.side[kk] ? h : jj) : h;
-                const int th = u ? (a.side[kk] ? jj : tt) : tt;
-                ent = role ? th : hh;
-                slot = (kk * 2 + u) * 2 + role;
-            }
-        } else if (pq < npairs) {
-            ent = r;  // entityVec_next_[relation] (transr/trainer.cpp:187)
-            slot = -2;
-        }
-        if (pq < PP) {
-            ent_of[pq] = ent;
-            slot_of[pq] = slot;
-        }
-        wave_lds_sync();
-        bool dup = false;
-        for (int k = 0; k < PP; k += 4) {  // PP is a multiple of 16
-            const int4 e4 = *(const int4*)(ent_of + k);
-            dup |= (k < pq && e4.x == ent) | (k + 1 < pq && e4.y == ent) | (k + 2 < pq && e4.z == ent) |
-                   (k + 3 < pq && e4.w == ent);
-        }
-        const bool live = ent >= 0 && !dup;
-        const uint64_t m = __ballot(live);
-        const int pos = __builtin_popcountll(m & ((1ull << l) - 1));
-        if (live) rowmap[pos] = pq;
-        if (pq < PP) posmap[pq] = live ? pos : -1;
-        // a pair without a row of its own (inactive slot, repeated entity) has no record
-        if (pq < 4 * cnt && slot >= 0 && !live) bf.pflag[slot] = 0;
-        if (l < 8) misc[l] = l == 0 ? __builtin_popcountll(m) : 0;
+        if (l < 8) misc[l] = 0;
     } else {
         // W0 as element pairs (ld is even and the row padding is zero), every
         // load of the thread in flight before the first LDS store
@@ -292,30 +262,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
             if (idx < kPairs) ((T2*)Wl)[idx] = v[q];
         }
     }
-    __syncthreads();  // W0 and the pair rows are in place
+    __syncthreads();  // W0 in place
     const unsigned long long ck1 = bf.stats ? clock64() : 0ull;
-    const int nrows = misc[0];
-    const int nblk = (nrows + 15) >> 4;
-    const bool mine = w < nblk;  // this wave owns pair rows [16 w, 16 w + 16)
-    const int row = w * 16 + l16;
     T ps[NS], gs[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) ps[s] = gs[s] = T(0);
     T c2 = T(0);
     bool lv = false;
-    int sl = -1;
     uint32_t vm16 = 0;
     if (mine) {
-        const int e = row < nrows ? ent_of[rowmap[row]] : -1;
-        // a0 rows straight into B fragments (not kept: the matrix partial
-        // re-reads them), |a0|^2, then P0^T = W0^T A0^T and the check
-        const T* ar = bf.ent + (int64_t)(e < 0 ? 0 : e) * ld;
-        T af[KS];
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {  // unconditional loads (in-row index), masked by a
-            const int k = kmap<T>(s, kq);  // product: a select lets the compiler branch around each load
-            af[s] = ar[k < n ? k : 0] * ((e >= 0 && k < n) ? T(1) : T(0));
-        }
+        // |a0|^2, then P0^T = W0^T A0^T and the check
         T ss = T(0);
 #pragma unroll
         for (int s = 0; s < KS; ++s) ss += af[s] * af[s];
@@ -332,7 +288,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
 #pragma unroll
         for (int s = 0; s < KS; ++s) nr0 += ps[s] * ps[s];
         lv = row < nrows && row4_sum(nr0) > T(1);
-        sl = row < nrows ? slot_of[rowmap[row]] : -1;
         if (kq == 0 && sl >= 0) bf.pflag[sl] = lv ? 1 : 0;
         vm16 = (uint32_t)__ballot(lv) & 0xFFFFu;  // lanes 0-15: one per row
         if (vm16 && l == 0) {
@@ -455,7 +410,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int rq = w * 16 + q;
-                const int eq = rq < nrows ? ent_of[rowmap[rq]] : 0;
+                const int eq = rq < nrows ? readlane_i32(e, q) : 0;  // lane q holds row 16 w + q
                 a0v[q] = bf.ent[(int64_t)eq * ld + (l < n ? l : 0)] * ((rq < nrows && l < n) ? T(1) : T(0));
             }
             if (l < NP)

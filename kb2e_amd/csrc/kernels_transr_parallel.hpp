@@ -81,11 +81,19 @@ struct RParBufs {
     uint8_t* pflag;      // [B][2][2] the pair record of the slot is valid this batch
     int32_t* cons_tile;  // [tiles][cons_ppt] the transRNorm matrix partial is valid (0: none)
     int32_t cons_ppt;    // transRNorm matrix partials per tile (1, or one per row block)
+    // register-fragment kernels (kernels_transr_wave.hpp): phase A's entity of every
+    // (tile, V row) and the transRNorm pairs of every tile, compacted by the gradient
+    // kernel: [tile][kCPairs] entities then [tile][kCPairs] slots, and the row count
+    int32_t* trow;       // [tiles][32]
+    int32_t* cpairs;     // [tiles][2][kCPairs]
+    int32_t* cnrows;     // [tiles]
     int32_t stats;       // count transRNorm rounds (tools)
     int32_t dbg;         // transRNorm wave kernel: phases skipped for timing experiments (tools; wrong results)
 };
 
 __host__ __device__ constexpr int rm_up16_host_dev(int v) { return (v + 15) & ~15; }
+constexpr int kTRows = 32;   // V rows of a tile on the register-fragment path (4 St, St <= 8)
+constexpr int kCPairs = 64;  // transRNorm pairs of a tile (4 St + 1 <= 64)
 
 template <typename T>
 __host__ __device__ constexpr int rpar_lds_w(int n, int ld) {

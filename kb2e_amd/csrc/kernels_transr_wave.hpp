@@ -63,6 +63,7 @@ __global__ __launch_bounds__(128) void transr_proj_wave_kernel(RParArgs a, RParB
     const int h = a.heads[i0], tt = a.tails[i0];
     const bool sd = a.side[kk] != 0;
     const int e = which == 0 ? h : which == 1 ? tt : which == 2 ? (sd ? h : jj) : (sd ? jj : tt);
+    if (kq == 0) bf.trow[blockIdx.x * kTRows + w * 16 + l16] = has ? e : -1;  // for the transRNorm pairs
     {  // W0 as element pairs, every load in flight before the LDS stores
         using T2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
         constexpr int kPairs = NP * L / 2, kThreads = kProjWaves * kWave;
@@ -213,6 +214,52 @@ __global__ __launch_bounds__(256) void transr_grad_wave_kernel(RParArgs a, RParB
         int nact = 0;
         for (int u = 0; u < nu; ++u) nact += a.act[a.kl.kk_of(a.keys[e0 + u])] != 0;
         a.tile_act[t] = nact;
+    }
+    if (w == kConsWaves - 1) {
+        // the tile's transRNorm pairs for transr_cons_wave_kernel: (h', r), (t', r) of the
+        // active updates in (sample, update, role) order -- phase A's V rows -- then
+        // (entity'[r], r) on the relation's first tile if any of its samples is active;
+        // first occurrences only, compacted; pairs without a row get pflag 0
+        __shared__ int ents[kCPairs];
+        const RTile tl = a.tiles[t];
+        bool relpair = false;
+        if (tl.q == 0 && r < a.ne) {
+            const int p0 = a.seg_start[tl.seg], ns = (a.seg_start[tl.seg + 1] - p0) / 2;
+            for (int m0 = 0; m0 < ns && !relpair; m0 += kWave)
+                relpair = __ballot(m0 + l < ns && a.act[a.kl.kk_of(a.keys[p0 + 2 * (m0 + l)])]) != 0;
+        }
+        const int pq = l;
+        int ent = -1, slot = -1;
+        if (pq < 4 * cnt) {
+            const int q = pq >> 2, u = (pq >> 1) & 1, role = pq & 1;
+            const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
+            if (a.act[kk]) {
+                ent = bf.trow[blockIdx.x * kTRows + pq];
+                slot = (kk * 2 + u) * 2 + role;
+            }
+        } else if (pq == 4 * cnt && relpair) {
+            ent = r;  // entityVec_next_[relation] (transr/trainer.cpp:187)
+            slot = -2;
+        }
+        ents[pq] = ent;
+        wave_lds_sync();
+        bool dup = false;
+        for (int k = 0; k < kCPairs; k += 4) {
+            const int4 e4 = *(const int4*)(ents + k);
+            dup |= (k < pq && e4.x == ent) | (k + 1 < pq && e4.y == ent) | (k + 2 < pq && e4.z == ent) |
+                   (k + 3 < pq && e4.w == ent);
+        }
+        const bool live = ent >= 0 && !dup;
+        const uint64_t m = __ballot(live);
+        const int pos = __builtin_popcountll(m & ((1ull << l) - 1));
+        int32_t* cp = bf.cpairs + (int64_t)blockIdx.x * 2 * kCPairs;
+        if (live) {
+            cp[pos] = ent;
+            cp[kCPairs + pos] = slot;
+        } else if (slot >= 0) {
+            bf.pflag[slot] = 0;
+        }
+        if (l == 0) bf.cnrows[blockIdx.x] = __builtin_popcountll(m);
     }
 }
 
