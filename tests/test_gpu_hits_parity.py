@@ -16,7 +16,7 @@ Bars (BASELINE.json north_star: "matching Hits@10(Filter) +-0.5"):
   * the ORDERED run learns: filtered Hits@10 >= 10x random (10 / |E|) for
     TransE, TransH and TransR with the zeroed (fixed) energy.
 For scale: two ORDERED runs that differ only in the glibc seed land
-0.17-0.28 pp apart on this set (tools/hits_sweep.py, profiles/hits_parity_r10.md).
+0.17-0.28 pp apart on this set (tools/hits_sweep.py, profiles/hits_sweep_r10_small.jsonl).
 
 TransR compat (the reference's accumulating work-vector energy,
 transr/transr.cpp:20-25) does not learn under the reference's own algorithm:
