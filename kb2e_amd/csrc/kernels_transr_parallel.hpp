@@ -741,24 +741,36 @@ static __attribute__((unused)) __global__ __launch_bounds__(256) void rpar_scan_
 // and the hinge (common/trainer.cpp:138-141).  The last chunk leaves the work
 // vectors after the batch in work_out (ping-pong with work_in across batches).
 template <typename T>
-__global__ __launch_bounds__(256) void rpar_scan_energy_kernel(RParArgs a, RParBufs<T> bf, const double* sums,
-                                                               int32_t nchunks, const double* work_in,
-                                                               double* work_out) {
+__global__ __launch_bounds__(1024) void rpar_scan_energy_kernel(RParArgs a, RParBufs<T> bf, const double* sums,
+                                                                int32_t nchunks, const double* work_in,
+                                                                double* work_out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double* run_l = (double*)smem;  // [kScanChunk][2 n]
     const int c = blockIdx.x, n = a.n, ld = a.ld;
     const int64_t calls = 2 * (int64_t)a.B;
     const int64_t c0 = (int64_t)c * kScanChunk, c1 = min<int64_t>(calls, c0 + kScanChunk);
-    for (int e = threadIdx.x; e < 2 * n; e += blockDim.x) {
+    // the sums of all earlier chunks: G thread groups per element, group g over chunks
+    // g*16.., (g+G)*16.., sixteen loads in flight (one round trip for FB15k's ~150
+    // chunks instead of ten), combined in group order
+    const int E2 = 2 * n, G = max(1, (int)blockDim.x / E2);
+    double* part = run_l + kScanChunk * E2;  // [G][2 n]
+    if ((int)threadIdx.x < G * E2) {
+        const int g = threadIdx.x / E2, e = threadIdx.x % E2;
         double s[4] = {0, 0, 0, 0};
-        for (int q0 = 0; q0 < c; q0 += 16) {
+        for (int q0 = g * 16; q0 < c; q0 += G * 16) {
             double v[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = q0 + q < c ? sums[(int64_t)(q0 + q) * 2 * n + e] : 0.0;
+            for (int q = 0; q < 16; ++q) v[q] = q0 + q < c ? sums[(int64_t)(q0 + q) * E2 + e] : 0.0;
 #pragma unroll
             for (int q = 0; q < 16; ++q) s[q & 3] += v[q];
         }
-        double run = work_in[e] + ((s[0] + s[1]) + (s[2] + s[3]));
+        part[g * E2 + e] = (s[0] + s[1]) + (s[2] + s[3]);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 2 * n; e += blockDim.x) {
+        double pre = 0.0;
+        for (int g = 0; g < G; ++g) pre += part[g * E2 + e];
+        double run = work_in[e] + pre;
         const int side = e / n, i = e % n;
         for (int64_t k = c0; k < c1; k += 16) {
             double v[16];
