@@ -53,9 +53,13 @@ kb2e_amd/libkb2e.so: kb2e_amd/build/engine.o kb2e_amd/build/eval.o kb2e_amd/buil
 # diagnostic build: per-phase cycle counters in the relation-owner kernels
 prof: kb2e_amd/libkb2e_prof.so
 
-kb2e_amd/libkb2e_prof.so: $(CSRC) kb2e_amd/build/eval.o kb2e_amd/build/textio.o kb2e_amd/build/transr_cons.o
-	$(HIPCC) $(HIPFLAGS) -DKB2E_OWNER_PROF -shared -o $@ kb2e_amd/csrc/engine.hip kb2e_amd/build/eval.o \
-	    kb2e_amd/build/textio.o kb2e_amd/build/transr_cons.o
+kb2e_amd/build/engine_prof.o: $(CSRC)
+	@mkdir -p kb2e_amd/build
+	$(HIPCC) $(HIPFLAGS) -DKB2E_OWNER_PROF -c -o $@ kb2e_amd/csrc/engine.hip
+
+kb2e_amd/libkb2e_prof.so: kb2e_amd/build/engine_prof.o kb2e_amd/build/eval.o kb2e_amd/build/textio.o \
+		kb2e_amd/build/transr_cons.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 oracle:
 	$(MAKE) -C oracle all
