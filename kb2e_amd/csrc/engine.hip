@@ -1452,15 +1452,6 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
             std::memset(fp, 0, sizeof(fp));
             HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_fold_prof), fp, sizeof(fp)));
             HIPCHK(hipMemcpyFromSymbol(fp[0], HIP_SYMBOL(g_long_prof), sizeof(fp[0])));
-            {
-                unsigned long long op[16];
-                HIPCHK(hipMemcpyFromSymbol(op, HIP_SYMBOL(g_orth_prof), sizeof(op)));
-                fprintf(stderr, "orth_prof tasks %llu wswitch %llu chunks %llu passes %llu | cycles all %llu passsetup %llu "
-                        "taskbuild %llu wload %llu normorth %llu waitA+other %llu loopmisc %llu\n", op[0], op[1], op[2],
-                        op[3], op[4], op[5], op[6], op[7], op[8], op[14], op[15]);
-                std::memset(op, 0, sizeof(op));
-                HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_orth_prof), op, sizeof(op)));
-            }
             fprintf(stderr, "long_prof");
             for (int k = 0; k < 16; ++k) fprintf(stderr, " %llu", fp[0][k]);
             fprintf(stderr, "\n");

@@ -193,107 +193,14 @@ struct PendingRows {
     }
 };
 
-// common/utils.cpp:79-111 norm(a, b, rate) with the loop carried on scalars.
-// After the leading unit norm of b (a vector operation, as written), every
-// iterate is a combination a = p a0 + q b0, b = u a0 + v b0 of the rows that
-// entered the loop, so |b|^2 and x = a.b follow from the three Gram products
-// a0.a0, a0.b0, b0.b0 (one wave reduction for the three): an iteration is a
-// dozen dependent scalar operations instead of two wave reductions, a sqrt
-// and 2n divisions.  The reference's running `sum` (never reset) is kept.
-// The rows are formed once at the end, then the trailing unit norm of b.
-// Values agree with the element-wise loop to rounding (~1e-15 relative;
-// PARALLEL-schedule tolerance, tests/test_gpu_parallel.py); every decision
-// x > 0.1 is the same unless x lies within that rounding of 0.1.
-template <typename T, int CH>
-__device__ __forceinline__ void orth_norm_gram(RowReg<T, CH>& A, RowReg<T, CH>& Bv, int n, T rate, bool unit) {
-    // unit: Bv is the previous call's output (just scaled to unit length): the
-    // leading norm would divide by 1 +- ulp, skipped
-    if (!unit) Bv.norm(n, false);
-    T g[3] = {T(0), T(0), T(0)};
-#pragma unroll
-    for (int c = 0; c < CH; ++c)
-#pragma unroll
-        for (int k = 0; k < kVec; ++k) {
-            g[0] += A.v[c][k] * A.v[c][k];
-            g[1] += A.v[c][k] * Bv.v[c][k];
-            g[2] += Bv.v[c][k] * Bv.v[c][k];
-        }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) g[i] = wave_sum(g[i]);
-    const T aa = g[0], ab = g[1], bb = g[2];
-    T p = T(1), q = T(0), u = T(0), v = T(1), sum = T(0);
-    bool moved = false;
-    for (int it = 0; it < 1 << 20; ++it) {
-        sum = sqrt(sum + ((u * u) * aa + T(2) * (u * v) * ab + (v * v) * bb));
-        const T rs = T(1) / sum;
-        u = u * rs;
-        v = v * rs;
-        const T x = (p * u) * aa + (p * v + q * u) * ab + (q * v) * bb;
-        if (!(x > T(0.1))) break;
-        moved = true;
-        p = p - rate * u;  // a -= rate b
-        q = q - rate * v;
-        u = u - rate * p;  // b -= rate a
-        v = v - rate * q;
-    }
-#pragma unroll
-    for (int c = 0; c < CH; ++c)
-#pragma unroll
-        for (int k = 0; k < kVec; ++k) {
-            if (!elem_valid(c, k, n)) continue;
-            const T a0 = A.v[c][k], b0 = Bv.v[c][k];
-            if (moved) A.v[c][k] = p * a0 + q * b0;
-            Bv.v[c][k] = u * a0 + v * b0;
-        }
-    Bv.norm(n, false);
-}
-
-// The rows of the flagged pairs are prefetched kOrthAhead tasks ahead (a task =
-// one flagged (row, w) pair, in sample order); a row that one of the last
-// kOrthAhead tasks stored is taken from those tasks' register copies instead
-// of the (possibly stale) prefetch, and a prefetch of a row stored earlier and
-// not yet drained waits for the stores first (PendingRows) -- so the serial
-// part per task is normOrth itself, not a memory round trip.
-constexpr int kOrthAhead = 4;
-#ifdef KB2E_OWNER_PROF
-__device__ unsigned long long g_orth_prof[16];  // tasks, w switches, chunks, passes, cycles: all, pass setup, task build, w loads, normOrth
-#define ORTH_PROF(k, v) (l == 0 ? (void)atomicAdd(&g_orth_prof[k], (unsigned long long)(v)) : (void)0)
-#else
-#define ORTH_PROF(k, v) ((void)0)
-#endif
-
 template <typename T, int CH>
 __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
     __shared__ int list[8 * kWave * kOrthWords];
-    __shared__ int tkey[6 * kWave], trel[6 * kWave];  // the chunk's tasks: row key, relation
     const int l = lane_id();
     RowReg<T, CH> W;
     int wid = -1;
-    bool wunit = false;  // W holds the last normOrth's unit output
     PendingRows pend;
-    // ids: relations [0, nr), w rows [nr, 2 nr), entities from 2 nr
-    auto row_of = [&](int key) -> T* {
-        return key < a.nr ? a.rel + (int64_t)key * a.ld : a.ent + (int64_t)(key - 2 * a.nr) * a.ld;
-    };
-#ifdef KB2E_OWNER_PROF
-    const unsigned long long ckA = clock64();
-    unsigned long long ck = ckA;
-#else
-    unsigned long long ck = 0;
-#endif
-    auto mark = [&](int k) {
-#ifdef KB2E_OWNER_PROF
-        const unsigned long long c2 = clock64();
-        ORTH_PROF(k, c2 - ck);
-        ck = c2;
-#else
-        (void)k;
-        (void)ck;
-#endif
-    };
     for (int base = 0; base < a.B; base += 8 * kWave * kOrthWords) {
-        ORTH_PROF(3, 1);
-        mark(15);
         uint64_t word[kOrthWords];
 #pragma unroll
         for (int wi = 0; wi < kOrthWords; ++wi) {  // orth_mask is zero past B up to a multiple of 512
@@ -319,118 +226,53 @@ __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
             count += __shfl(pre, kWave - 1);
         }
         wave_lds_sync();
-        mark(5);
         for (int g = 0; g < count; g += kWave) {
-            ORTH_PROF(2, 1);
-            // this lane's list entry: its flagged rows become tasks, in (sample, q) order
-            int ntask;
-            {
-                int bits = 0, ids[6] = {0, 0, 0, 0, 0, 0}, r = 0;
-                if (g + l < count) {
-                    const int k2 = list[g + l];
-                    const int i0 = a.si[k2], j = a.sj[k2];
-                    const bool sd = a.side[k2];
-                    bits = a.orth_mask[k2];
-                    const int h = a.heads[i0], t = a.tails[i0];
-                    r = a.rels[i0];
-                    ids[0] = r;
-                    ids[1] = 2 * a.nr + h;
-                    ids[2] = 2 * a.nr + t;
-                    ids[3] = r;
-                    ids[4] = 2 * a.nr + (sd ? h : j);
-                    ids[5] = 2 * a.nr + (sd ? j : t);
-                }
-                const int mine = __builtin_popcount(bits & 63);
-                int pre = mine;
-#pragma unroll
-                for (int d = 1; d < kWave; d <<= 1) {
-                    const int v = __shfl_up(pre, d);
-                    if (l >= d) pre += v;
-                }
-                int pos = pre - mine;
-#pragma unroll
-                for (int q = 0; q < 6; ++q)
-                    if ((bits >> q) & 1) {
-                        tkey[pos] = ids[q];
-                        trel[pos] = r;
-                        ++pos;
-                    }
-                ntask = __shfl(pre, kWave - 1);
+            int k2 = -1, r = 0, h = 0, t = 0, nh = 0, nt = 0, bits = 0;
+            if (g + l < count) {  // this lane's list entry: ids from the sample stream
+                k2 = list[g + l];
+                const int i0 = a.si[k2], j = a.sj[k2];
+                const bool sd = a.side[k2];
+                bits = a.orth_mask[k2];
+                h = a.heads[i0];
+                t = a.tails[i0];
+                r = a.rels[i0];
+                nh = sd ? h : j;
+                nt = sd ? j : t;
             }
-            wave_lds_sync();
-            mark(6);
-            ORTH_PROF(0, ntask);
-            // prefetch ring: slot j holds task t0 + j's row (t0 a multiple of kOrthAhead)
-            RowReg<T, CH> ring[kOrthAhead], done[kOrthAhead];
-            int dkey[kOrthAhead];
-#pragma unroll
-            for (int j = 0; j < kOrthAhead; ++j) {
-                dkey[j] = -1;
-                if (j < ntask) {
-                    const int key = tkey[j];
+            const int ng = min(kWave, count - g);
+            for (int e = 0; e < ng; ++e) {
+                const uint32_t eb = (uint32_t)readlane_i32(bits, e);
+                const int er = readlane_i32(r, e);
+                const int ids[6] = {er, readlane_i32(h, e), readlane_i32(t, e), er, readlane_i32(nh, e),
+                                    readlane_i32(nt, e)};
+                if (er != wid) {  // w_r: kept in registers while consecutive samples share the relation
+                    if (wid >= 0) {
+                        row_store_sc1(W, a.w + (int64_t)wid * a.ld, a.n);
+                        pend.add(a.nr + wid);
+                    }
+                    pend.before_load(a.nr + er);
+                    row_load_sc1(W, a.w + (int64_t)er * a.ld, a.n);
+                    wid = er;
+                }
+                for (int q = 0; q < 6; ++q) {
+                    if (!((eb >> q) & 1u)) continue;
+                    const bool isrel = q == 0 || q == 3;
+                    T* row = (isrel ? a.rel : a.ent) + (int64_t)ids[q] * a.ld;
+                    // ids: relations [0, nr), w rows [nr, 2 nr), entities from 2 nr
+                    const int key = isrel ? ids[q] : 2 * a.nr + ids[q];
+                    RowReg<T, CH> A;
                     pend.before_load(key);
-                    row_load_sc1(ring[j], row_of(key), a.n);
-                }
-            }
-            for (int t0 = 0; t0 < ntask; t0 += kOrthAhead) {
-#pragma unroll
-                for (int j = 0; j < kOrthAhead; ++j) {
-                    const int t = t0 + j;
-                    if (t >= ntask) break;
-                    const int key = tkey[t], er = trel[t];
-                    if (er != wid) {  // w_r: kept in registers while consecutive tasks share the relation
-                        mark(14);
-                        ORTH_PROF(1, 1);
-                        if (wid >= 0) {
-                            row_store_sc1(W, a.w + (int64_t)wid * a.ld, a.n);
-                            pend.add(a.nr + wid);
-                        }
-                        pend.before_load(a.nr + er);
-                        row_load_sc1(W, a.w + (int64_t)er * a.ld, a.n);
-                        wid = er;
-                        wunit = false;
-#ifdef KB2E_OWNER_PROF
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-                        mark(7);
-                    }
-                    // the row: the newest copy among the last kOrthAhead tasks' stores, else the prefetch
-                    RowReg<T, CH> A = ring[j];
-#pragma unroll
-                    for (int d = 1; d <= kOrthAhead; ++d) {  // slot (j - d) mod kOrthAhead: task t - d
-                        const int sd = (j - d + kOrthAhead) % kOrthAhead;
-                        if (dkey[sd] == key && t - d >= 0) {
-                            A = done[sd];
-                            break;
-                        }
-                    }
-#ifdef KB2E_OWNER_PROF
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-                    mark(14);
-                    orth_norm_gram<T, CH>(A, W, a.n, (T)a.lr, wunit);
-                    wunit = true;
-                    mark(8);
-                    row_store_sc1(A, row_of(key), a.n);
+                    row_load_sc1(A, row, a.n);
+                    orth_norm<T, CH>(A, W, a.n, (T)a.lr);
+                    row_store_sc1(A, row, a.n);
                     pend.add(key);
-                    done[j] = A;
-                    dkey[j] = key;
-                    if (t + kOrthAhead < ntask) {  // the prefetch of task t + kOrthAhead into the freed slot
-                        const int k2 = tkey[t + kOrthAhead];
-                        pend.before_load(k2);
-                        row_load_sc1(ring[j], row_of(k2), a.n);
-                    }
                 }
             }
-            wave_lds_sync();
         }
         wave_lds_sync();
     }
     if (wid >= 0) row_store_sc1(W, a.w + (int64_t)wid * a.ld, a.n);
     drain_stores();
-#ifdef KB2E_OWNER_PROF
-    ORTH_PROF(4, clock64() - ckA);
-#endif
 }
 
 }  // namespace kb2e
