@@ -70,7 +70,7 @@ void check_dataflow(kb2e_ctx* c);
 void build_owner_index(kb2e_ctx* c);
 void prepare_relowner_kernels();
 void setup_transr_parallel(kb2e_ctx* c);
-void build_transr_tiles(kb2e_ctx* c, bool tiles);
+void build_transr_tiles(kb2e_ctx* c, bool tiles, hipStream_t st);
 template <typename T>
 void run_batch_transr_parallel(kb2e_ctx* c, int64_t b);
 template <typename T, int CH>
@@ -105,6 +105,10 @@ struct kb2e_ctx {
     // made on the host, the rejection chain is resolved on the device.
     hipStream_t side_stream = nullptr;
     DevBuf words, levels, jfin, sidefin, filter_slots, pr_dev, consumed_dev;
+    DevBuf trip;  // int4 per training triple: head, tail, relation, Bernoulli threshold (sample_len)
+    DevBuf glibc_pow;  // M^(2^k) of the kGlibcBlock-word jump (glibc_starts_pow_kernel)
+    DevBuf chain_table, chain_super, chain_sc, chain_ch, chain_overflow;  // the chain by chunks
+    bool sampler_doubling = false;  // a sample longer than kChainEmax words was seen: pointer doubling
     int64_t* pin_consumed = nullptr;
     uint32_t* pin_win = nullptr;            // generator window after the epoch (31 words)
     DevBuf raw_words, glibc_starts, glibc_table, win_dev;
@@ -112,6 +116,11 @@ struct kb2e_ctx {
     double words_per_sample = 6.0;
     bool prefetch_valid = false;   // set cur^1 holds the stream for the current rng state
     uint64_t rng_version = 0, prefetch_version = 0;
+    // PARALLEL schedule: the next epoch's event index is built on the side stream
+    // right after its sample stream, into the shadow buffers (sh_*), and swapped in
+    // at the epoch boundary (swap_index) -- no index build on the batches' stream
+    int64_t prefetch_gen = 0, committed_gen = -1, index_pre_gen = -2;
+    hipEvent_t ev_index = nullptr;
     hipEvent_t ev_sampled = nullptr, ev_epoch_done = nullptr;
     bool host_sampler = false;     // KB2E_HOST_SAMPLER=1: draw on the host (debug)
     // replay stream supplied by the caller
@@ -152,6 +161,9 @@ struct kb2e_ctx {
     hipStream_t fold_stream = nullptr;  // the long-segment fold runs beside the per-row fold
     hipEvent_t ev_fold_a = nullptr, ev_fold_b = nullptr;
     DevBuf long_list, long_count;
+    DevBuf sh_keys, sh_keys_sorted, sh_sort_tmp, sh_flags, sh_idx, sh_seg_start, sh_nseg, sh_nvalid, sh_batch_seg,
+        sh_ev_slot_sorted, sh_ev_inv, sh_seg_row, sh_rpar_ntiles, sh_rpar_rel_begin, sh_rpar_tile_first,
+        sh_rpar_tiles, sh_par_long_list, sh_par_long_count;
     // stats
     DevBuf stats;  // double loss, double active (reduced)
     double acc_loss = 0;
@@ -182,6 +194,7 @@ struct kb2e_ctx {
         flush_timers();
         if (ev_sampled) (void)hipEventDestroy(ev_sampled);
         if (ev_epoch_done) (void)hipEventDestroy(ev_epoch_done);
+        if (ev_index) (void)hipEventDestroy(ev_index);
         if (side_stream) (void)hipStreamDestroy(side_stream);
         if (fold_stream) (void)hipStreamDestroy(fold_stream);
         if (ev_fold_a) (void)hipEventDestroy(ev_fold_a);
@@ -356,15 +369,42 @@ void upload_tables(kb2e_ctx* c, const double* e, const double* r, const double* 
 
 // ------------------------------------------------------------------- index
 
-void build_index(kb2e_ctx* c) {
+// The index buffers of one epoch (build_index writes them; the batches read them).
+std::vector<std::pair<DevBuf*, DevBuf*>> index_bufs(kb2e_ctx* c) {
+    return {{&c->keys, &c->sh_keys}, {&c->keys_sorted, &c->sh_keys_sorted}, {&c->sort_tmp, &c->sh_sort_tmp},
+            {&c->flags, &c->sh_flags}, {&c->idx, &c->sh_idx}, {&c->seg_start, &c->sh_seg_start},
+            {&c->nseg, &c->sh_nseg}, {&c->nvalid, &c->sh_nvalid}, {&c->batch_seg, &c->sh_batch_seg},
+            {&c->ev_slot_sorted, &c->sh_ev_slot_sorted}, {&c->ev_inv, &c->sh_ev_inv}, {&c->seg_row, &c->sh_seg_row},
+            {&c->rpar_ntiles, &c->sh_rpar_ntiles}, {&c->rpar_rel_begin, &c->sh_rpar_rel_begin},
+            {&c->rpar_tile_first, &c->sh_rpar_tile_first}, {&c->rpar_tiles, &c->sh_rpar_tiles},
+            {&c->par_long_list, &c->sh_par_long_list}, {&c->par_long_count, &c->sh_par_long_count}};
+}
+
+void swap_index(kb2e_ctx* c) {
+    for (auto& pr : index_bufs(c)) {
+        std::swap(pr.first->p, pr.second->p);
+        std::swap(pr.first->bytes, pr.second->bytes);
+    }
+}
+
+void alloc_shadow_index(kb2e_ctx* c) {
+    for (auto& pr : index_bufs(c)) {
+        pr.second->free();
+        if (pr.first->p) pr.second->alloc(pr.first->bytes);
+    }
+    c->index_pre_gen = -2;
+}
+
+// The epoch index of sample-stream set `set`, on stream st (timed on the batches' stream).
+void build_index(kb2e_ctx* c, hipStream_t st, int set) {
     const int64_t nkeys = c->S * c->slots;
     KeyArgs ka{};
     ka.heads = c->heads.as<int32_t>();
     ka.tails = c->tails.as<int32_t>();
     ka.rels = c->rels.as<int32_t>();
-    ka.si = c->si();
-    ka.sj = c->sj();
-    ka.side = c->side();
+    ka.si = c->si_[set].as<int32_t>();
+    ka.sj = c->sj_[set].as<int32_t>();
+    ka.side = c->side_[set].as<uint8_t>();
     ka.owner = c->cfg.model == KB2E_TRANSE ? nullptr : c->owner.as<int32_t>();
     ka.nsamples = c->S;
     ka.B = (int32_t)c->B;
@@ -372,55 +412,57 @@ void build_index(kb2e_ctx* c) {
     ka.kl = c->kl;
     ka.keys = c->keys.as<uint64_t>();
     const int grid = (int)((c->S + 255) / 256);
-    c->timed("index", [&] {
+    auto build = [&] {
         if (c->cfg.model == KB2E_TRANSR)
-            emit_keys_kernel<8, true><<<grid, 256, 0, c->stream>>>(ka);
+            emit_keys_kernel<8, true><<<grid, 256, 0, st>>>(ka);
         else
-            emit_keys_kernel<6, false><<<grid, 256, 0, c->stream>>>(ka);
+            emit_keys_kernel<6, false><<<grid, 256, 0, st>>>(ka);
         HIPCHK(hipGetLastError());
         size_t tb = c->sort_tmp_bytes;
         if (c->parallel()) {  // the sorted position of every emitted key, for phase A's event records
             HIPCHK(hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tb, c->keys.as<uint64_t>(),
                                                       c->keys_sorted.as<uint64_t>(), c->ev_iota.as<int32_t>(),
                                                       c->ev_slot_sorted.as<int32_t>(), (int)nkeys, 0,
-                                                      c->kl.total_bits(), c->stream));
-            inverse_perm_kernel<<<(int)((nkeys + 255) / 256), 256, 0, c->stream>>>(c->ev_slot_sorted.as<int32_t>(),
+                                                      c->kl.total_bits(), st));
+            inverse_perm_kernel<<<(int)((nkeys + 255) / 256), 256, 0, st>>>(c->ev_slot_sorted.as<int32_t>(),
                                                                                   nkeys, c->ev_inv.as<int32_t>());
             HIPCHK(hipGetLastError());
         } else {
             HIPCHK(hipcub::DeviceRadixSort::SortKeys(c->sort_tmp.p, tb, c->keys.as<uint64_t>(),
                                                      c->keys_sorted.as<uint64_t>(), (int)nkeys, 0,
-                                                     c->kl.total_bits(), c->stream));
+                                                     c->kl.total_bits(), st));
         }
         const int g2 = (int)((nkeys + 255) / 256);
-        seg_flags_kernel<<<g2, 256, 0, c->stream>>>(c->keys_sorted.as<uint64_t>(), nkeys, c->kl,
+        seg_flags_kernel<<<g2, 256, 0, st>>>(c->keys_sorted.as<uint64_t>(), nkeys, c->kl,
                                                      c->flags.as<int32_t>(), c->nvalid.as<int32_t>());
         HIPCHK(hipGetLastError());
         tb = c->sort_tmp_bytes;
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, tb, c->flags.as<int32_t>(),
-                                                c->idx.as<int32_t>(), (int)nkeys, c->stream));
-        seg_scatter_kernel<<<g2, 256, 0, c->stream>>>(c->flags.as<int32_t>(), c->idx.as<int32_t>(), nkeys,
+                                                c->idx.as<int32_t>(), (int)nkeys, st));
+        seg_scatter_kernel<<<g2, 256, 0, st>>>(c->flags.as<int32_t>(), c->idx.as<int32_t>(), nkeys,
                                                        c->seg_start.as<int32_t>(), c->nseg.as<int32_t>(),
                                                        c->nvalid.as<int32_t>());
         HIPCHK(hipGetLastError());
-        batch_begin_kernel<<<256, 256, 0, c->stream>>>(c->keys_sorted.as<uint64_t>(), c->seg_start.as<int32_t>(),
+        batch_begin_kernel<<<256, 256, 0, st>>>(c->keys_sorted.as<uint64_t>(), c->seg_start.as<int32_t>(),
                                                         c->nseg.as<int32_t>(), (int)c->nb, c->kl,
                                                         c->batch_seg.as<int32_t>());
         HIPCHK(hipGetLastError());
         if (c->cfg.model != KB2E_TRANSE && !c->parallel()) build_owner_index(c);
         if (c->parallel()) {
-            seg_rows_kernel<<<256, 256, 0, c->stream>>>(c->keys_sorted.as<uint64_t>(), c->seg_start.as<int32_t>(),
+            seg_rows_kernel<<<256, 256, 0, st>>>(c->keys_sorted.as<uint64_t>(), c->seg_start.as<int32_t>(),
                                                        c->nseg.as<int32_t>(), c->kl, c->seg_row.as<int32_t>());
             HIPCHK(hipGetLastError());
-            if (c->cfg.model != KB2E_TRANSE) build_transr_tiles(c, c->cfg.model == KB2E_TRANSR);
+            if (c->cfg.model != KB2E_TRANSE) build_transr_tiles(c, c->cfg.model == KB2E_TRANSR, st);
         }
         if (c->cfg.model != KB2E_TRANSR && c->cfg.schedule == KB2E_SCHEDULE_PARALLEL && c->apply_long_min > 0) {
-            long_lists_kernel<<<(int)c->nb, 1024, 0, c->stream>>>(
+            long_lists_kernel<<<(int)c->nb, 1024, 0, st>>>(
                 c->seg_start.as<int32_t>(), c->batch_seg.as<int32_t>(), c->apply_long_min, c->par_long_cap,
                 c->par_long_list.as<int32_t>(), c->par_long_count.as<int32_t>());
             HIPCHK(hipGetLastError());
         }
-    });
+    };
+    if (st == c->stream) c->timed("index", build);
+    else build();
 }
 
 // ----------------------------------------------------------------- sampling
@@ -440,6 +482,12 @@ void ensure_sampler_capacity(kb2e_ctx* c, int64_t nraw) {
     c->sidefin.alloc(nraw);
     c->raw_words.alloc((nraw + GlibcRand::kDeg) * 4);
     c->glibc_starts.alloc(((nraw + kGlibcBlock - 1) / kGlibcBlock) * GlibcRand::kDeg * 4);
+    const int64_t nchunks = (nraw + kChainW - 1) / kChainW, nsuper = (nchunks + kChainG - 1) / kChainG;
+    c->chain_table.alloc((size_t)nchunks * 64 * 4);
+    c->chain_super.alloc((size_t)nsuper * 64 * 8);
+    c->chain_sc.alloc((size_t)nsuper * 8);
+    c->chain_ch.alloc((size_t)nchunks * 8);
+    c->chain_overflow.alloc(16);
     c->nraw_cap = nraw;
 }
 
@@ -450,6 +498,23 @@ void ensure_jump_table(kb2e_ctx* c) {
     glibc_jump_table(kGlibcBlock, C.data());
     c->glibc_table.alloc(C.size() * 4);
     HIPCHK(hipMemcpy(c->glibc_table.p, C.data(), C.size() * 4, hipMemcpyHostToDevice));
+    // M (the window after kGlibcBlock words from the window before) and its squares
+    constexpr int D = GlibcRand::kDeg;
+    std::vector<uint32_t> P((size_t)kGlibcPowLevels * D * D);
+    for (int j = 0; j < D; ++j)
+        for (int m = 0; m < D; ++m) P[(size_t)j * D + m] = C[(size_t)m * kGlibcBlock + (kGlibcBlock - D + j)];
+    for (int k = 1; k < kGlibcPowLevels; ++k) {
+        const uint32_t* A = P.data() + (size_t)(k - 1) * D * D;
+        uint32_t* Q = P.data() + (size_t)k * D * D;
+        for (int i = 0; i < D; ++i)
+            for (int j = 0; j < D; ++j) {
+                uint32_t v = 0;
+                for (int m = 0; m < D; ++m) v += A[i * D + m] * A[m * D + j];
+                Q[i * D + j] = v;
+            }
+    }
+    c->glibc_pow.alloc(P.size() * 4);
+    HIPCHK(hipMemcpy(c->glibc_pow.p, P.data(), P.size() * 4, hipMemcpyHostToDevice));
 }
 
 // Draw the stream of the epoch that follows the committed rng state into set
@@ -469,8 +534,11 @@ void launch_prefetch(kb2e_ctx* c) {
     HIPCHK(hipStreamWaitEvent(st, c->ev_epoch_done, 0));
     {
         const int64_t nblocks = (nraw + kGlibcBlock - 1) / kGlibcBlock;
-        glibc_starts_kernel<<<1, 64, 0, st>>>(win, c->glibc_table.as<uint32_t>(), kGlibcBlock, (int32_t)nblocks,
-                                              c->glibc_starts.as<uint32_t>(), c->raw_words.as<uint32_t>());
+        if (nblocks >= (int64_t)1 << kGlibcPowLevels) throw std::runtime_error("sampler word buffer too large");
+        glibc_starts_pow_kernel<<<(int)nblocks, 64, 0, st>>>(win, c->glibc_pow.as<uint32_t>(),
+                                                             c->glibc_starts.as<uint32_t>(),
+                                                             c->raw_words.as<uint32_t>(),
+                                                             c->chain_overflow.as<int32_t>());
         HIPCHK(hipGetLastError());
         glibc_words_kernel<<<(int)((nraw + 255) / 256), 256, 0, st>>>(
             c->glibc_table.as<uint32_t>(), kGlibcBlock, c->glibc_starts.as<uint32_t>(), nraw,
@@ -481,12 +549,9 @@ void launch_prefetch(kb2e_ctx* c) {
     SamplerArgs a{};
     a.words = c->words.as<int32_t>();
     a.nraw = nraw;
-    a.heads = c->heads.as<int32_t>();
-    a.tails = c->tails.as<int32_t>();
-    a.rels = c->rels.as<int32_t>();
+    a.trip = c->trip.as<int4>();
     a.ntrain = (int32_t)c->ts.size();
     a.ne = c->cfg.num_entities;
-    a.pr = c->pr_dev.as<double>();
     a.slots = c->filter_slots.as<uint64_t>();
     a.mask = c->ts.filter.mask;
     a.nr64 = (uint64_t)c->cfg.num_relations;
@@ -495,9 +560,40 @@ void launch_prefetch(kb2e_ctx* c) {
     a.jfin = c->jfin.as<int32_t>();
     a.sidefin = c->sidefin.as<uint8_t>();
     const int64_t stride = nraw + 1;
+    const bool doubling = c->sampler_doubling || getenv("KB2E_SAMPLER_DOUBLING");
     auto launch = [&] {
         sample_len_kernel<<<(int)((stride + 255) / 256), 256, 0, st>>>(a);
         HIPCHK(hipGetLastError());
+        if (!doubling) {
+            ChunkArgs ch{};
+            ch.next = a.next;
+            ch.nraw = nraw;
+            ch.nchunks = (int32_t)((nraw + kChainW - 1) / kChainW);
+            ch.nsuper = (ch.nchunks + kChainG - 1) / kChainG;
+            const char* em = getenv("KB2E_SAMPLER_EMAX");  // tests: a low limit forces the overflow path
+            ch.emax = em ? std::max(1, std::min(kChainEmax, atoi(em))) : kChainEmax;
+            ch.table = c->chain_table.as<uint32_t>();
+            ch.super = c->chain_super.as<uint2>();
+            ch.sc_state = c->chain_sc.as<uint2>();
+            ch.ch_state = c->chain_ch.as<uint2>();
+            ch.overflow = c->chain_overflow.as<int32_t>();
+            ch.nsamples = c->S;
+            ch.words = a.words;
+            ch.jfin = a.jfin;
+            ch.sidefin = a.sidefin;
+            ch.ntrain = a.ntrain;
+            ch.si = c->si_[set].as<int32_t>();
+            ch.sj = c->sj_[set].as<int32_t>();
+            ch.side = c->side_[set].as<uint8_t>();
+            ch.consumed = c->consumed_dev.as<int64_t>();
+            chain_table_kernel<<<ch.nchunks, 64, 0, st>>>(ch);
+            chain_super_kernel<<<ch.nsuper, 64, 0, st>>>(ch);
+            chain_top_kernel<<<1, 64, 0, st>>>(ch);
+            chain_entries_kernel<<<ch.nsuper, 64, 0, st>>>(ch);
+            chain_emit_kernel<<<ch.nchunks, 256, 0, st>>>(ch);
+            HIPCHK(hipGetLastError());
+            return;
+        }
         for (int k = 1; k < K; ++k) {
             sample_double_kernel<<<(int)((stride + 255) / 256), 256, 0, st>>>(
                 c->levels.as<int32_t>() + (int64_t)(k - 1) * stride, c->levels.as<int32_t>() + (int64_t)k * stride,
@@ -539,6 +635,7 @@ void launch_prefetch(kb2e_ctx* c) {
     HIPCHK(hipEventRecord(c->ev_sampled, st));
     c->prefetch_valid = true;
     c->prefetch_version = c->rng_version;
+    c->prefetch_gen++;
 }
 
 // Make set `cur` hold this epoch's stream and commit the rng past it.
@@ -558,6 +655,7 @@ void start_epoch_stream(kb2e_ctx* c) {
             c->rng_version++;
         }
         // the previous epoch may still read set cur: use the other set
+        c->committed_gen = -1;
         c->cur ^= 1;
         upload_stream(c, c->cur, c->stream);
         HIPCHK(hipStreamSynchronize(c->stream));  // pinned buffers are reused next epoch
@@ -567,6 +665,11 @@ void start_epoch_stream(kb2e_ctx* c) {
         if (!c->prefetch_valid || c->prefetch_version != c->rng_version) launch_prefetch(c);
         HIPCHK(hipEventSynchronize(c->ev_sampled));
         const int64_t used = *c->pin_consumed;
+        if (used == -2) {  // a sample longer than the chunked chain tabulates: redraw by doubling
+            c->sampler_doubling = true;
+            c->prefetch_valid = false;
+            continue;
+        }
         if (used >= 0) {
             c->rng.set_window(c->pin_win);  // the generator after the epoch's `used` words
             c->rng_version++;
@@ -580,6 +683,7 @@ void start_epoch_stream(kb2e_ctx* c) {
             throw std::runtime_error("negative sampler cannot terminate: every entity completes a training triple");
     }
     c->prefetch_valid = false;
+    c->committed_gen = c->prefetch_gen;  // the prefetch this epoch consumes
     c->cur ^= 1;
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_sampled, 0));
     // Draw the next epoch's stream now, beside this epoch's batches: it writes
@@ -847,7 +951,22 @@ void run_batches(kb2e_ctx* c, int64_t count) {
     for (int64_t q = 0; q < count; ++q) {
         if (c->epoch_pos == 0 && !c->epoch_ready) {
             start_epoch_stream(c);
-            build_index(c);
+            if (c->committed_gen >= 0 && c->index_pre_gen == c->committed_gen) {
+                HIPCHK(hipStreamWaitEvent(c->stream, c->ev_index, 0));  // built beside the previous epoch
+                swap_index(c);
+            } else {
+                build_index(c, c->stream, c->cur);
+            }
+            if (c->parallel() && c->prefetch_valid && c->sh_keys.p) {
+                // the next epoch's index beside this epoch's batches, right after its
+                // sample stream (same side stream); it overwrites the set the previous
+                // epoch read, which the prefetch already waited for (ev_epoch_done)
+                swap_index(c);
+                build_index(c, c->side_stream, c->cur ^ 1);
+                swap_index(c);
+                HIPCHK(hipEventRecord(c->ev_index, c->side_stream));
+                c->index_pre_gen = c->prefetch_gen;
+            }
             c->epoch_ready = true;
             c->reduced_upto = 0;
         }
@@ -978,6 +1097,7 @@ void setup_epoch_buffers(kb2e_ctx* c) {
         c->rpar_ntiles.alloc((size_t)(nkeys + 1) * 4);
         c->rpar_rel_begin.alloc((size_t)c->nb * 4);
     }
+    if (c->parallel() && !getenv("KB2E_NO_PREINDEX")) alloc_shadow_index(c);  // the prebuilt next-epoch index
     c->device_bytes = 0;
     for (DevBuf* d : {&c->ent, &c->rel, &c->w, &c->heads, &c->tails, &c->rels, &c->si_[0], &c->sj_[0], &c->side_[0],
                       &c->si_[1], &c->sj_[1], &c->side_[1], &c->filter_slots, &c->pr_dev,
@@ -1089,6 +1209,7 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
         HIPCHK(hipEventCreateWithFlags(&c->ev_fold_b, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->ev_sampled, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->ev_epoch_done, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_index, hipEventDisableTiming));
         HIPCHK(hipEventRecord(c->ev_epoch_done, c->stream));
         HIPCHK(hipDeviceGetAttribute(&c->num_cus, hipDeviceAttributeMultiprocessorCount, g.device));
         prepare_relowner_kernels();
@@ -1133,6 +1254,23 @@ kb2e_status kb2e_upload_triples(kb2e_ctx* c, const int32_t* h, const int32_t* t,
         if (c->cfg.method == 0) std::fill(pr.begin(), pr.end(), 500.0);  // common/trainer.cpp:84-86
         c->pr_dev.alloc(pr.size() * 8);
         HIPCHK(hipMemcpy(c->pr_dev.p, pr.data(), pr.size() * 8, hipMemcpyHostToDevice));
+        {  // sample_len's packed triples: (double)(rand() % 1000) < pr[r] <=> rand() % 1000 < thr[r]
+            std::vector<int32_t> thr(pr.size());
+            for (size_t q = 0; q < pr.size(); ++q) {
+                int32_t k = 0;
+                while (k < 1000 && (double)k < pr[q]) ++k;
+                thr[q] = k;
+            }
+            std::vector<int32_t> tp((size_t)count * 4);
+            for (int64_t q = 0; q < count; ++q) {
+                tp[4 * q] = h[q];
+                tp[4 * q + 1] = t[q];
+                tp[4 * q + 2] = r[q];
+                tp[4 * q + 3] = thr[r[q]];
+            }
+            c->trip.alloc(tp.size() * 4);
+            HIPCHK(hipMemcpy(c->trip.p, tp.data(), tp.size() * 4, hipMemcpyHostToDevice));
+        }
         if (c->cfg.model != KB2E_TRANSE && c->parallel()) {
             // PARALLEL TransH/TransR: every relation is its own event row
             c->plan.num_owners = c->cfg.num_relations;

@@ -21,7 +21,7 @@ struct GlibcWindow {
     uint32_t w[31];
 };
 
-__global__ __launch_bounds__(64) void glibc_starts_kernel(GlibcWindow win, const uint32_t* C, int32_t L,
+[[maybe_unused]] __global__ __launch_bounds__(64) void glibc_starts_kernel(GlibcWindow win, const uint32_t* C, int32_t L,
                                                           int32_t nblocks, uint32_t* starts, uint32_t* raw) {
     __shared__ uint32_t cur[32];
     __shared__ uint32_t tail[31][32];  // tail[j][m] = C[m][L - 31 + j]
@@ -46,6 +46,40 @@ __global__ __launch_bounds__(64) void glibc_starts_kernel(GlibcWindow win, const
         if (l < 31) cur[l] = v;
         __syncthreads();
     }
+}
+
+// glibc_starts_pow: the same windows with no walk: the window before block p is
+//   M^p applied to the starting window (M = the L-word jump, rows L-31..L-1 of
+//   the table), one workgroup per block multiplying by the precomputed squares
+//   M^(2^k) of p's set bits (row-major 31 x 31, k < kGlibcPowLevels).  Block 0
+//   also writes raw[0..31) and clears *clear (the sampler's overflow flag).
+constexpr int kGlibcPowLevels = 24;
+
+[[maybe_unused]] __global__ __launch_bounds__(64) void glibc_starts_pow_kernel(GlibcWindow win, const uint32_t* P,
+                                                                              uint32_t* starts, uint32_t* raw,
+                                                                              int32_t* clear) {
+    __shared__ uint32_t cur[32];
+    const int l = threadIdx.x;
+    const int p = blockIdx.x;
+    if (l < 31) cur[l] = win.w[l];
+    if (p == 0) {
+        if (l < 31) raw[l] = win.w[l];
+        if (l == 0 && clear) *clear = 0;
+    }
+    __syncthreads();
+    for (int k = 0; (p >> k) != 0; ++k) {
+        if (!((p >> k) & 1)) continue;
+        uint32_t v = 0;
+        if (l < 31) {
+            const uint32_t* row = P + ((size_t)k * 31 + l) * 31;
+#pragma unroll
+            for (int m = 0; m < 31; ++m) v += row[m] * cur[m];
+        }
+        __syncthreads();
+        if (l < 31) cur[l] = v;
+        __syncthreads();
+    }
+    if (l < 31) starts[(size_t)p * 31 + l] = cur[l];
 }
 
 __global__ __launch_bounds__(256) void glibc_words_kernel(const uint32_t* C, int32_t L, const uint32_t* starts,

@@ -10,11 +10,20 @@
 // and the filter, never on embeddings, so:
 //   1. sample_len: every word position p computes the sample that would start
 //      there (filter probes included) -> next[p], j[p], side[p]   (parallel);
-//   2. pointer doubling: level k holds next^(2^k)                  (log S passes);
-//   3. sample_chain: sample s starts at next^s(0), composed from the levels;
-//   4. sample_emit: (i, j, side) of every sample + the words consumed.
-// The host supplies the raw words (glibc TYPE_3 outputs) of the epoch and
-// advances its own generator by exactly the number consumed.
+//   2. the chain by chunks (chain_*): the stream is cut into chunks of kChainW
+//      words; a sample chain enters a chunk at an offset below the previous
+//      sample's length, so each chunk tabulates, per entry offset < kChainEmax,
+//      where the chain leaves it and how many samples it starts there; the
+//      tables compose (superchunks of kChainG chunks, then one walk over the
+//      superchunks) into every chunk's true entry and first sample index, and
+//      each chunk emits its samples.  A sample longer than kChainEmax words at a
+//      chunk edge flags overflow (consumed = -2) and the host redraws the epoch
+//      with the general form:
+//   2'. pointer doubling: level k holds next^(2^k) (log S passes), sample s
+//      starts at next^s(0), composed from the levels (sample_chain).
+// The device makes the raw words (glibc TYPE_3 outputs) of the epoch from the
+// generator's window; the host advances its generator by exactly the number
+// consumed.
 #pragma once
 
 #include "kernels_common.hpp"
@@ -25,11 +34,9 @@ namespace kb2e {
 struct SamplerArgs {
     const int32_t* words;   // rand() outputs, [nraw]
     int64_t nraw;
-    const int32_t* heads;
-    const int32_t* tails;
-    const int32_t* rels;
+    const int4* trip;       // per training triple: head, tail, relation, Bernoulli threshold
+                            // (#k in [0,1000) with k < pr[r], pr = 1000*tailMean/(tailMean+headMean) or 500)
     int32_t ntrain, ne;
-    const double* pr;       // per relation: 1000*tailMean/(tailMean+headMean), or 500 (unif)
     const uint64_t* slots;  // filter hash table
     uint64_t mask;
     uint64_t nr64, ne64;
@@ -81,10 +88,10 @@ __global__ __launch_bounds__(256) void sample_len_kernel(SamplerArgs a) {
     const int32_t* w = a.words;
     const int32_t i = dev_rand_max(w[p], w[p + 1], a.ntrain);
     int32_t j = dev_rand_max(w[p + 2], w[p + 3], a.ne);
-    const int32_t r = a.rels[i];
-    const bool tail = (double)(w[p + 4] % 1000) < a.pr[r];
+    const int4 tr = a.trip[i];  // one line for the triple and its threshold
+    const int32_t h = tr.x, t = tr.y, r = tr.z;
+    const bool tail = w[p + 4] % 1000 < tr.w;  // == (double)(rand() % 1000) < pr[r]
     int64_t q = p + 5;
-    const int32_t h = a.heads[i], t = a.tails[i];
     uint8_t valid = 1;
     while (tail ? filter_has(a, h, r, j) : filter_has(a, j, r, t)) {
         if (q + 2 > a.nraw) {  // words ran out inside the rejection loop
@@ -136,6 +143,174 @@ __global__ __launch_bounds__(256) void sample_chain_kernel(ChainArgs a) {
     a.side[s] = ok ? a.sidefin[p] : 0;
     // Chain positions increase, so the last sample is valid iff all are.
     if (s == a.nsamples - 1) *a.consumed = ok ? (int64_t)a.next[p] : -1;
+}
+
+// ---------------------------------------------------------------- the chain by chunks
+constexpr int kChainW = 1024;           // words per chunk
+constexpr int kChainEmax = 64;          // entry offsets tabulated per chunk
+constexpr int kChainG = 64;             // chunks per superchunk
+constexpr int kChainMaxSamples = kChainW / 5 + 2;  // samples are >= 5 words long
+constexpr uint32_t kChainTerm = 255;    // the chain has ended (reached nraw)
+
+struct ChunkArgs {
+    const int32_t* next;    // sample_len's next[], [nraw + 1]
+    int64_t nraw;
+    int32_t nchunks, nsuper;
+    int32_t emax;           // entry offsets allowed (<= kChainEmax; lower only to test the overflow path)
+    uint32_t* table;        // [nchunks][64]: exit offset | samples << 8
+    uint2* super;           // [nsuper][64]: (exit offset, samples)
+    uint2* sc_state;        // [nsuper]: (entry offset, first sample)
+    uint2* ch_state;        // [nchunks]
+    int32_t* overflow;      // cleared by glibc_starts_pow_kernel
+    // emission, as sample_chain
+    int64_t nsamples;
+    const int32_t* words;
+    const int32_t* jfin;
+    const uint8_t* sidefin;
+    int32_t ntrain;
+    int32_t* si;
+    int32_t* sj;
+    uint8_t* side;
+    int64_t* consumed;
+};
+
+// Per chunk and entry offset e (one lane each): walk next[] in LDS from the
+// chunk's word e to the first chain position past the chunk.
+__global__ __launch_bounds__(64) void chain_table_kernel(ChunkArgs a) {
+    __shared__ int32_t nx[kChainW];
+    const int c = blockIdx.x, l = threadIdx.x;
+    const int64_t base = (int64_t)c * kChainW;
+    const int64_t end = min(base + kChainW, a.nraw);
+    for (int q = l; q < kChainW; q += 64) {
+        const int64_t p = base + q;
+        nx[q] = p < a.nraw ? a.next[p] : (int32_t)a.nraw;
+    }
+    __syncthreads();
+    int64_t p = base + l;
+    uint32_t cnt = 0;
+    while (p < end) {  // next[p] > p: the walk ends
+        ++cnt;
+        p = nx[p - base];
+    }
+    uint32_t ex = kChainTerm;
+    if (p < a.nraw) {
+        const int64_t e = p - (base + kChainW);
+        if (e < a.emax) ex = (uint32_t)e;
+        else a.overflow[0] = 1;
+    }
+    a.table[(size_t)c * 64 + l] = ex | cnt << 8;
+}
+
+// Per superchunk: the composed table of its kChainG chunks, every entry offset a lane.
+__global__ __launch_bounds__(64) void chain_super_kernel(ChunkArgs a) {
+    __shared__ uint32_t T[kChainG][64];
+    const int sc = blockIdx.x, l = threadIdx.x;
+    const int c0 = sc * kChainG, ng = min(kChainG, a.nchunks - c0);
+    for (int g = 0; g < ng; ++g) T[g][l] = a.table[(size_t)(c0 + g) * 64 + l];
+    __syncthreads();
+    uint32_t cur = l, tot = 0;
+    for (int g = 0; g < ng && cur != kChainTerm; ++g) {
+        const uint32_t v = T[g][cur];
+        tot += v >> 8;
+        cur = v & 255;
+    }
+    a.super[(size_t)sc * 64 + l] = make_uint2(cur, tot);
+}
+
+// One workgroup: the chain through the superchunks from word 0 (tiles of 64
+// superchunk tables in LDS, one lane walking); the error words of consumed.
+__global__ __launch_bounds__(64) void chain_top_kernel(ChunkArgs a) {
+    __shared__ uint2 T[64][64];
+    __shared__ uint32_t s_cur, s_base;
+    const int l = threadIdx.x;
+    if (l == 0) {
+        s_cur = 0;
+        s_base = 0;
+    }
+    for (int t0 = 0; t0 < a.nsuper; t0 += 64) {
+        const int nt = min(64, a.nsuper - t0);
+        __syncthreads();
+        for (int g = 0; g < nt; ++g) T[g][l] = a.super[(size_t)(t0 + g) * 64 + l];
+        __syncthreads();
+        if (l == 0) {
+            uint32_t cur = s_cur, base = s_base;
+            for (int g = 0; g < nt; ++g) {
+                a.sc_state[t0 + g] = make_uint2(cur, base);
+                if (cur != kChainTerm) {
+                    const uint2 v = T[g][cur];
+                    base += v.y;
+                    cur = v.x;
+                }
+            }
+            s_cur = cur;
+            s_base = base;
+        }
+    }
+    __syncthreads();
+    if (l == 0) {
+        if (a.overflow[0]) *a.consumed = -2;                       // redraw with pointer doubling
+        else if ((int64_t)s_base < a.nsamples) *a.consumed = -1;  // the word buffer ran out
+    }
+}
+
+// Per superchunk: each chunk's entry offset and first sample, from the superchunk's.
+__global__ __launch_bounds__(64) void chain_entries_kernel(ChunkArgs a) {
+    __shared__ uint32_t T[kChainG][64];
+    const int sc = blockIdx.x, l = threadIdx.x;
+    const int c0 = sc * kChainG, ng = min(kChainG, a.nchunks - c0);
+    for (int g = 0; g < ng; ++g) T[g][l] = a.table[(size_t)(c0 + g) * 64 + l];
+    __syncthreads();
+    if (l == 0) {
+        const uint2 st = a.sc_state[sc];
+        uint32_t cur = st.x, base = st.y;
+        for (int g = 0; g < ng; ++g) {
+            a.ch_state[c0 + g] = make_uint2(cur, base);
+            if (cur != kChainTerm) {
+                const uint32_t v = T[g][cur];
+                base += v >> 8;
+                cur = v & 255;
+            }
+        }
+    }
+}
+
+// Per chunk: the chain's positions in it (one lane walks LDS), then every
+// sample written by its own lane (as sample_chain_kernel).
+__global__ __launch_bounds__(256) void chain_emit_kernel(ChunkArgs a) {
+    __shared__ int32_t nx[kChainW];
+    __shared__ int32_t pos[kChainMaxSamples];
+    __shared__ int32_t s_cnt;
+    const int c = blockIdx.x, l = threadIdx.x;
+    const uint2 st = a.ch_state[c];
+    if (a.overflow[0] || st.x == kChainTerm || (int64_t)st.y >= a.nsamples) return;
+    const int64_t base = (int64_t)c * kChainW;
+    const int64_t end = min(base + kChainW, a.nraw);
+    for (int q = l; q < kChainW; q += 256) {
+        const int64_t p = base + q;
+        nx[q] = p < a.nraw ? a.next[p] : (int32_t)a.nraw;
+    }
+    __syncthreads();
+    if (l == 0) {
+        int64_t p = base + st.x;
+        int k = 0;
+        while (p < end) {
+            pos[k++] = (int32_t)p;
+            p = nx[p - base];
+        }
+        s_cnt = k;
+    }
+    __syncthreads();
+    const int cnt = s_cnt;
+    for (int k = l; k < cnt; k += 256) {
+        const int64_t s = (int64_t)st.y + k;
+        if (s >= a.nsamples) break;
+        const int32_t p = pos[k];
+        const bool ok = a.sidefin[p] != 2;
+        a.si[s] = ok ? dev_rand_max(a.words[p], a.words[p + 1], a.ntrain) : 0;
+        a.sj[s] = ok ? a.jfin[p] : 0;
+        a.side[s] = ok ? a.sidefin[p] : 0;
+        if (s == a.nsamples - 1) *a.consumed = ok ? (int64_t)a.next[p] : -1;
+    }
 }
 
 }  // namespace kb2e
