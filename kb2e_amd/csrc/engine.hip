@@ -120,6 +120,7 @@ struct kb2e_ctx {
     // right after its sample stream, into the shadow buffers (sh_*), and swapped in
     // at the epoch boundary (swap_index) -- no index build on the batches' stream
     int64_t prefetch_gen = 0, committed_gen = -1, index_pre_gen = -2;
+    bool next_pending = false;  // launch_next after the epoch's first batch
     hipEvent_t ev_index = nullptr;
     hipEvent_t ev_sampled = nullptr, ev_epoch_done = nullptr;
     bool host_sampler = false;     // KB2E_HOST_SAMPLER=1: draw on the host (debug)
@@ -418,18 +419,22 @@ void build_index(kb2e_ctx* c, hipStream_t st, int set) {
         else
             emit_keys_kernel<6, false><<<grid, 256, 0, st>>>(ka);
         HIPCHK(hipGetLastError());
+        // Keys are emitted sample-major and, within one sample and row, in (u, roles)
+        // order, so a stable radix sort on the [batch | row] bits alone gives the
+        // full-key order (sentinels stay last: batch nb-1 is never all-ones).
+        const int lo_bit = getenv("KB2E_SORT_FULLKEY") ? 0 : c->kl.row_shift();
         size_t tb = c->sort_tmp_bytes;
         if (c->parallel()) {  // the sorted position of every emitted key, for phase A's event records
             HIPCHK(hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tb, c->keys.as<uint64_t>(),
                                                       c->keys_sorted.as<uint64_t>(), c->ev_iota.as<int32_t>(),
-                                                      c->ev_slot_sorted.as<int32_t>(), (int)nkeys, 0,
+                                                      c->ev_slot_sorted.as<int32_t>(), (int)nkeys, lo_bit,
                                                       c->kl.total_bits(), st));
             inverse_perm_kernel<<<(int)((nkeys + 255) / 256), 256, 0, st>>>(c->ev_slot_sorted.as<int32_t>(),
                                                                                   nkeys, c->ev_inv.as<int32_t>());
             HIPCHK(hipGetLastError());
         } else {
             HIPCHK(hipcub::DeviceRadixSort::SortKeys(c->sort_tmp.p, tb, c->keys.as<uint64_t>(),
-                                                     c->keys_sorted.as<uint64_t>(), (int)nkeys, 0,
+                                                     c->keys_sorted.as<uint64_t>(), (int)nkeys, lo_bit,
                                                      c->kl.total_bits(), st));
         }
         const int g2 = (int)((nkeys + 255) / 256);
@@ -562,7 +567,10 @@ void launch_prefetch(kb2e_ctx* c) {
     const int64_t stride = nraw + 1;
     const bool doubling = c->sampler_doubling || getenv("KB2E_SAMPLER_DOUBLING");
     auto launch = [&] {
-        sample_len_kernel<<<(int)((stride + 255) / 256), 256, 0, st>>>(a);
+        const char* sg = getenv("KB2E_SAMPLE_GRID");
+        const int64_t g_full = (stride + 255) / 256;
+        sample_len_kernel<<<(int)(sg ? std::max<int64_t>(1, std::min<int64_t>(g_full, atoi(sg))) : g_full), 256, 0,
+                            st>>>(a);
         HIPCHK(hipGetLastError());
         if (!doubling) {
             ChunkArgs ch{};
@@ -686,10 +694,26 @@ void start_epoch_stream(kb2e_ctx* c) {
     c->committed_gen = c->prefetch_gen;  // the prefetch this epoch consumes
     c->cur ^= 1;
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_sampled, 0));
-    // Draw the next epoch's stream now, beside this epoch's batches: it writes
-    // the set the previous epoch read (the side stream waits for that epoch's
-    // end marker) and its rng start is this epoch's committed end.
+    // The next epoch's stream is drawn beside this epoch's batches (launch_next,
+    // once the epoch's first batch is queued): it writes the set the previous
+    // epoch read (the side stream waits for that epoch's end marker) and its rng
+    // start is this epoch's committed end.
+    c->next_pending = true;
+}
+
+// The next epoch's sample stream and (PARALLEL) its event index, on the side stream.
+void launch_next(kb2e_ctx* c) {
+    c->next_pending = false;
     launch_prefetch(c);
+    if (c->parallel() && c->sh_keys.p) {
+        // into the shadow index buffers (the set the previous epoch read, which the
+        // prefetch already waited for), right after the sample stream
+        swap_index(c);
+        build_index(c, c->side_stream, c->cur ^ 1);
+        swap_index(c);
+        HIPCHK(hipEventRecord(c->ev_index, c->side_stream));
+        c->index_pre_gen = c->prefetch_gen;
+    }
 }
 
 // --------------------------------------------------------------- the batch
@@ -957,16 +981,6 @@ void run_batches(kb2e_ctx* c, int64_t count) {
             } else {
                 build_index(c, c->stream, c->cur);
             }
-            if (c->parallel() && c->prefetch_valid && c->sh_keys.p) {
-                // the next epoch's index beside this epoch's batches, right after its
-                // sample stream (same side stream); it overwrites the set the previous
-                // epoch read, which the prefetch already waited for (ev_epoch_done)
-                swap_index(c);
-                build_index(c, c->side_stream, c->cur ^ 1);
-                swap_index(c);
-                HIPCHK(hipEventRecord(c->ev_index, c->side_stream));
-                c->index_pre_gen = c->prefetch_gen;
-            }
             c->epoch_ready = true;
             c->reduced_upto = 0;
         }
@@ -983,6 +997,9 @@ void run_batches(kb2e_ctx* c, int64_t count) {
             c->epoch_pos = 0;
             c->epoch_ready = false;
         }
+        // after the epoch's first batch is queued: the GPU runs it while the host
+        // queues the side stream's work
+        if (c->next_pending) launch_next(c);
     }
 }
 
@@ -1024,6 +1041,7 @@ void setup_epoch_buffers(kb2e_ctx* c) {
         c->side_[q].alloc(c->S);
     }
     c->prefetch_valid = false;
+    c->next_pending = false;
     c->nraw_cap = 0;
     c->consumed_dev.alloc(16);
     if (!c->pin_consumed) HIPCHK(hipHostMalloc((void**)&c->pin_consumed, 16, 0));
@@ -1202,9 +1220,14 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
         HIPCHK(hipGetDeviceCount(&ndev));
         if (g.device < 0 || g.device >= ndev) return fail(c.get(), KB2E_EDEVICE, "no such HIP device");
         HIPCHK(hipSetDevice(g.device));
-        HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&c->fold_stream, hipStreamNonBlocking));
+        // the batches' streams high priority, the next epoch's sampling and index
+        // (side stream) low: its workgroups fill what the batches leave idle
+        int lo = 0, hi = 0;
+        const char* sp = getenv("KB2E_STREAM_PRIO");
+        if (!(sp && sp[0] == '0')) HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
+        HIPCHK(hipStreamCreateWithPriority(&c->side_stream, hipStreamNonBlocking, lo));
+        HIPCHK(hipStreamCreateWithPriority(&c->fold_stream, hipStreamNonBlocking, hi));
         HIPCHK(hipEventCreateWithFlags(&c->ev_fold_a, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->ev_fold_b, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->ev_sampled, hipEventDisableTiming));

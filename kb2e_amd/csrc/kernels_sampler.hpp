@@ -72,9 +72,17 @@ __device__ __forceinline__ int32_t dev_rand_max(int32_t a, int32_t b, int32_t x)
     return res;
 }
 
+__device__ __forceinline__ void sample_len_at(const SamplerArgs& a, int64_t p);
+
+// Grid-stride: the launch may use fewer workgroups than positions, so that
+// beside the batches (side stream) it holds a bounded share of the machine.
 __global__ __launch_bounds__(256) void sample_len_kernel(SamplerArgs a) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p > a.nraw) return;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= a.nraw;
+         p += (int64_t)gridDim.x * blockDim.x)
+        sample_len_at(a, p);
+}
+
+__device__ __forceinline__ void sample_len_at(const SamplerArgs& a, int64_t p) {
     if (p == a.nraw) {
         a.next[p] = (int32_t)a.nraw;  // sink
         return;
