@@ -4,7 +4,8 @@
 //
 // Same pairs and rules as transr_cons_tile_kernel (kernels_transr_mfma.hpp):
 // per tile, the (h', r), (t', r) pairs of its active updates and (entity'[r], r)
-// on the relation's first tile, first occurrences only; with W0 = W'_r,
+// on the relation's first tile, first occurrences per relation per batch only
+// (transr_pair_dup); with W0 = W'_r,
 // K = W0^T W0 and p = W0^T a0, while |p|^2 > 1:  G += 2 p,
 // p <- p - 2 lr K p - 2 lr |a0|^2 p, a row freezing at its own first
 // non-violation; then da = -lr W0 G (pair records) and dW = -lr a0 G^T (matrix

@@ -63,7 +63,24 @@ struct RParArgs {
     double* loss;        // [B]
     double* proj;        // [B][2][2][ld] compat projections
     int32_t* tile_act;   // [tiles] active updates per tile
+    const int32_t* pprev;  // [B][2][2] this batch's previous slot of the same (relation, entity) (pair_prev_kernel)
+    const int32_t* rlast;  // [nr] this batch's last slot whose entity is the relation id itself
 };
+
+// transRNorm pairs are deduplicated per relation per batch: a slot is skipped
+// when an earlier slot of an active sample holds the same (relation, entity);
+// (entity[r], r) when any active slot of relation r holds entity r.
+__device__ __forceinline__ bool transr_chain_active(const RParArgs& a, int s) {
+    for (; s >= 0; s = a.pprev[s])
+        if (a.act[s >> 2]) return true;
+    return false;
+}
+__device__ __forceinline__ bool transr_pair_dup(const RParArgs& a, int slot) {
+    return transr_chain_active(a, a.pprev[slot]);
+}
+__device__ __forceinline__ bool transr_relpair_dup(const RParArgs& a, int r) {
+    return transr_chain_active(a, a.rlast[r]);
+}
 
 template <typename T>
 struct RParBufs {
@@ -531,14 +548,14 @@ __global__ __launch_bounds__(256) void transr_constraint_kernel(RParArgs a, RPar
         if (pq < 4 * cnt) {
             const int q = pq >> 2, u = (pq >> 1) & 1, role = pq & 1;
             const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
-            if (a.act[kk]) {
+            if (a.act[kk] && !transr_pair_dup(a, (kk * 2 + u) * 2 + role)) {
                 const int i0 = a.si[kk], jj = a.sj[kk];
                 const int h = a.heads[i0], tt = a.tails[i0];
                 const int hh = u ? (a.side[kk] ? h : jj) : h;
                 const int th = u ? (a.side[kk] ? jj : tt) : tt;
                 ent = role ? th : hh;
             }
-        } else {
+        } else if (!transr_relpair_dup(a, r)) {
             ent = r;  // entityVec_next_[relation] (transr/trainer.cpp:187)
         }
         ent_of[pq] = ent;

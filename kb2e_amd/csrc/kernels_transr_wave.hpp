@@ -219,7 +219,9 @@ __global__ __launch_bounds__(256) void transr_grad_wave_kernel(RParArgs a, RParB
         // the tile's transRNorm pairs for transr_cons_wave_kernel: (h', r), (t', r) of the
         // active updates in (sample, update, role) order -- phase A's V rows -- then
         // (entity'[r], r) on the relation's first tile if any of its samples is active;
-        // first occurrences only, compacted; pairs without a row get pflag 0
+        // first occurrences per relation per batch only (transr_pair_dup: across the
+        // relation's tiles; the LDS check below catches nothing more), compacted;
+        // pairs without a row get pflag 0
         __shared__ int ents[kCPairs];
         const RTile tl = a.tiles[t];
         bool relpair = false;
@@ -234,10 +236,10 @@ __global__ __launch_bounds__(256) void transr_grad_wave_kernel(RParArgs a, RParB
             const int q = pq >> 2, u = (pq >> 1) & 1, role = pq & 1;
             const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
             if (a.act[kk]) {
-                ent = bf.trow[blockIdx.x * kTRows + pq];
                 slot = (kk * 2 + u) * 2 + role;
+                if (!transr_pair_dup(a, slot)) ent = bf.trow[blockIdx.x * kTRows + pq];
             }
-        } else if (pq == 4 * cnt && relpair) {
+        } else if (pq == 4 * cnt && relpair && !transr_relpair_dup(a, r)) {
             ent = r;  // entityVec_next_[relation] (transr/trainer.cpp:187)
             slot = -2;
         }

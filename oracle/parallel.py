@@ -144,46 +144,45 @@ def transr_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
     return loss, active
 
 
-def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St, dedupe=True, relpair=True, max_iter=256):
+def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, relpair=True, max_iter=256):
     """transRNorm step of the PARALLEL TransR schedule, in place.
 
-    Per tile (relation, St samples in kk order): pairs (h', r), (t', r) of the
-    active updates in (sample, update, role) order, then (entity'[r], r) on the
-    relation's first tile; first occurrences only; the loop in Jacobi form to
-    first order, iterated on the projection p = W^T a:
-    p <- p - 2 lr W^T W p - 2 lr |a0|^2 p, G += 2 p while |p|^2 > 1, then
-    da = -lr W G, dW = -lr a0 G^T (kernels_transr_mfma.hpp).
+    Per relation of the batch: pairs (h', r), (t', r) of the active updates in
+    (sample, update, role) order, then (entity'[r], r) (transr/trainer.cpp:187);
+    first occurrences per relation only (pair_prev_kernel, transr_pair_dup:
+    independent of how the GPU cuts the relation into tiles, so St is unused);
+    the loop in Jacobi form to first order, iterated on the projection
+    p = W^T a: p <- p - 2 lr W^T W p - 2 lr |a0|^2 p, G += 2 p while |p|^2 > 1,
+    then da = -lr W G, dW = -lr a0 G^T (kernels_transr_mfma.hpp).
     """
     ra = np.unique(r[act])
     W0 = W.copy()
     E1 = ent.copy()
     dWc = np.zeros_like(W)
     for rr in ra:
-        ks = np.nonzero(r == rr)[0]
-        for f in range(0, len(ks), St):
-            slots = []
-            for kk in ks[f:f + St]:
-                for (hh, tt) in ((h[kk], t[kk]), (nh[kk], nt[kk])):
-                    slots += [hh, tt] if act[kk] else [-1, -1]
-            if relpair and f == 0 and rr < ent.shape[0]:
-                slots.append(rr)
-            seen = set()
-            for e in slots:
-                if e < 0 or (dedupe and e in seen):
-                    continue
-                seen.add(e)
-                a0 = E1[e]
-                Wm = W0[rr]
-                G = np.zeros_like(a0)
-                s0 = a0 @ a0
-                p = Wm.T @ a0
-                for _ in range(max_iter):
-                    if not (p @ p > 1.0):
-                        break
-                    G += 2.0 * p
-                    p = p - 2.0 * rate * (Wm.T @ (Wm @ p)) - 2.0 * rate * s0 * p
-                ent[e] += -rate * (Wm @ G)
-                dWc[rr] += np.outer(-rate * a0, G)
+        slots = []
+        for kk in np.nonzero(r == rr)[0]:
+            for (hh, tt) in ((h[kk], t[kk]), (nh[kk], nt[kk])):
+                slots += [hh, tt] if act[kk] else [-1, -1]
+        if relpair and rr < ent.shape[0]:
+            slots.append(rr)
+        seen = set()
+        for e in slots:
+            if e < 0 or (dedupe and e in seen):
+                continue
+            seen.add(e)
+            a0 = E1[e]
+            Wm = W0[rr]
+            G = np.zeros_like(a0)
+            s0 = a0 @ a0
+            p = Wm.T @ a0
+            for _ in range(max_iter):
+                if not (p @ p > 1.0):
+                    break
+                G += 2.0 * p
+                p = p - 2.0 * rate * (Wm.T @ (Wm @ p)) - 2.0 * rate * s0 * p
+            ent[e] += -rate * (Wm @ G)
+            dWc[rr] += np.outer(-rate * a0, G)
     W[ra] += dWc[ra]
 
 
