@@ -139,6 +139,27 @@ def test_transr_parallel_compat(dim, St, mfma, monkeypatch):
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=True, mfma=mfma)
 
 
+def test_transr_parallel_independent_of_tile_size(monkeypatch):
+    """transRNorm pairs are deduplicated per relation per batch, so cutting the
+    relations into tiles of 1, 2 or 8 samples changes only the order of the
+    floating-point sums (the tile partials)."""
+    ds = tiny()
+    outs = []
+    for St in (1, 2, 8):
+        monkeypatch.setenv("KB2E_RPAR_ST", str(St))
+        eng = Engine("R", 20, ds.num_entities, ds.num_relations, rate=0.01, batches=10, seed=3,
+                     schedule="parallel")
+        eng.upload_triples(ds.train)
+        e0, r0, _ = eng.init_params()
+        eng.transr_seed(e0, r0)
+        stats = [eng.train_epoch() for _ in range(2)]
+        outs.append((stats, eng.download_params()))
+    for stats, tabs in outs[1:]:
+        assert [a for _, a in stats] == [a for _, a in outs[0][0]]
+        for x, y in zip(tabs, outs[0][1]):
+            assert max_abs(x, y) < 1e-12
+
+
 def test_transr_parallel_fp32_close(monkeypatch):
     """FP32 tables: hinge decisions flip at the margin, so statistics, not elements."""
     ds = tiny()
