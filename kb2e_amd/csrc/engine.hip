@@ -142,6 +142,7 @@ struct kb2e_ctx {
     DevBuf owner, tickets, ent_done, wsnap, transr_work, transr_work_alt, owner_seg, dataflow_err, wtouched, desc, cdesc, ocount;
     int num_cus = 256;
     uint32_t batch_stamp = 0;
+    uint32_t rpar_ptab_mask = 0;
     int32_t gram_min = 48;  // KB2E_GRAM_MIN: fold segments this long use the scalar recurrence (0 = off)
     int32_t long_min = 192;  // KB2E_FOLD_LONG: segments this long take the 4-wave fold (0 = off; L1 only)
     int32_t apply_long_min = 256;  // KB2E_APPLY_LONG: PARALLEL-schedule segments this long take a 16-wave workgroup
@@ -159,7 +160,7 @@ struct kb2e_ctx {
     DevBuf rpar_pflag, rpar_cons_tile, rpar_trow, rpar_cpairs, rpar_cnrows;
     DevBuf rpar_y, rpar_wpart, rpar_rpart, rpar_tile_act, rpar_pair, rpar_relpair, rpar_relpair_stamp, rpar_tiles,
         rpar_ntiles, rpar_tile_first, rpar_rel_begin, rpar_scan;
-    DevBuf rpar_pprev, rpar_rlast, sh_rpar_pprev, sh_rpar_rlast;  // transRNorm pair dedupe (pair_prev_kernel)
+    DevBuf rpar_ptab_keys, rpar_ptab_vals;  // transRNorm pair dedupe: per-batch (relation, entity) table
     hipStream_t fold_stream = nullptr;  // the long-segment fold runs beside the per-row fold
     hipEvent_t ev_fold_a = nullptr, ev_fold_b = nullptr;
     DevBuf long_list, long_count;
@@ -379,7 +380,7 @@ std::vector<std::pair<DevBuf*, DevBuf*>> index_bufs(kb2e_ctx* c) {
             {&c->ev_slot_sorted, &c->sh_ev_slot_sorted}, {&c->ev_inv, &c->sh_ev_inv}, {&c->seg_row, &c->sh_seg_row},
             {&c->rpar_ntiles, &c->sh_rpar_ntiles}, {&c->rpar_rel_begin, &c->sh_rpar_rel_begin},
             {&c->rpar_tile_first, &c->sh_rpar_tile_first}, {&c->rpar_tiles, &c->sh_rpar_tiles},
-            {&c->rpar_pprev, &c->sh_rpar_pprev}, {&c->rpar_rlast, &c->sh_rpar_rlast},
+
             {&c->par_long_list, &c->sh_par_long_list}, {&c->par_long_count, &c->sh_par_long_count}};
 }
 
@@ -460,22 +461,6 @@ void build_index(kb2e_ctx* c, hipStream_t st, int set) {
                                                        c->nseg.as<int32_t>(), c->kl, c->seg_row.as<int32_t>());
             HIPCHK(hipGetLastError());
             if (c->cfg.model != KB2E_TRANSE) build_transr_tiles(c, c->cfg.model == KB2E_TRANSR, st);
-            if (c->cfg.model == KB2E_TRANSR) {
-                PairPrevArgs pa{};
-                pa.keys = c->keys_sorted.as<uint64_t>();
-                pa.nvalid = c->nvalid.as<int32_t>();
-                pa.si = ka.si;
-                pa.rels = ka.rels;
-                pa.B = (int32_t)c->B;
-                pa.ne = c->cfg.num_entities;
-                pa.nr = c->cfg.num_relations;
-                pa.kl = c->kl;
-                pa.pprev = c->rpar_pprev.as<int32_t>();
-                pa.rlast = c->rpar_rlast.as<int32_t>();
-                HIPCHK(hipMemsetAsync(c->rpar_rlast.p, 0xff, c->rpar_rlast.bytes, st));
-                pair_prev_kernel<<<(int)((nkeys + 255) / 256), 256, 0, st>>>(pa);
-                HIPCHK(hipGetLastError());
-            }
         }
         if (c->cfg.model != KB2E_TRANSR && c->cfg.schedule == KB2E_SCHEDULE_PARALLEL && c->apply_long_min > 0) {
             long_lists_kernel<<<(int)c->nb, 1024, 0, st>>>(

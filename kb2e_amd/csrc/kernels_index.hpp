@@ -67,57 +67,6 @@ __global__ __launch_bounds__(256) void emit_keys_kernel(KeyArgs a) {
     while (w < SLOTS) out[w++] = kSentinelKey;
 }
 
-// PARALLEL TransR transRNorm pairs, deduplicated per relation per batch: for
-// every update slot s = (kk * 2 + u) * 2 + role (role 0 the update's head, 1 its
-// tail) the batch-local slot of the previous occurrence of the same (relation,
-// entity) in the relation's (sample, update, role) order, or -1; rlast[b][r] =
-// the last slot whose entity is r itself (the (entity[r], r) pair's duplicate,
-// transr/trainer.cpp:187).  From the sorted event index: an entity segment
-// lists the entity's events of one batch in (sample, update) order, so the
-// previous occurrence is the nearest earlier event of the segment whose sample
-// has the same relation.  Whether a slot is a duplicate then depends on which
-// samples are active (per batch): transr_pair_dup walks the chain.
-struct PairPrevArgs {
-    const uint64_t* keys;  // sorted
-    const int32_t* nvalid;
-    const int32_t* si;     // the epoch's sample stream
-    const int32_t* rels;
-    int32_t B, ne, nr;
-    KeyLayout kl;
-    int32_t* pprev;        // [S][2][2]
-    int32_t* rlast;        // [nb][nr], -1 before
-};
-
-__global__ __launch_bounds__(256) void pair_prev_kernel(PairPrevArgs a) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= *a.nvalid) return;
-    const uint64_t key = a.keys[p];
-    const int row = a.kl.row_of(key);
-    const uint32_t roles = (uint32_t)(key & 7);
-    const bool hd = roles & kRoleHead, tl = roles & kRoleTail;
-    if (row >= a.ne || !(hd || tl)) return;
-    const int b = a.kl.batch_of(key), kk = a.kl.kk_of(key), u = (int)((key >> 3) & 1);
-    const int64_t k0 = (int64_t)b * a.B;
-    const int rel = a.rels[a.si[k0 + kk]];
-    const uint64_t seg = a.kl.seg_part(key);
-    int prev = -1;
-    for (int64_t q = p - 1; q >= 0; --q) {
-        const uint64_t kq = a.keys[q];
-        if (a.kl.seg_part(kq) != seg) break;
-        const uint32_t rq = (uint32_t)(kq & 7);
-        if (!(rq & (kRoleHead | kRoleTail))) continue;
-        const int kkq = a.kl.kk_of(kq);
-        if (a.rels[a.si[k0 + kkq]] != rel) continue;
-        prev = (kkq * 2 + (int)((kq >> 3) & 1)) * 2 + ((rq & kRoleTail) ? 1 : 0);
-        break;
-    }
-    const int s0 = (kk * 2 + u) * 2;
-    int32_t* pp = a.pprev + (k0 + kk) * 4 + u * 2;
-    if (hd) pp[0] = prev;
-    if (tl) pp[1] = hd ? s0 : prev;
-    if (row == rel) atomicMax(a.rlast + (int64_t)b * a.nr + rel, s0 + (tl ? 1 : 0));
-}
-
 // flags[p] = 1 where a new (batch,row) segment starts; counts valid keys.
 __global__ __launch_bounds__(256) void seg_flags_kernel(const uint64_t* keys, int64_t n, KeyLayout kl,
                                                         int32_t* flags, int32_t* nvalid) {

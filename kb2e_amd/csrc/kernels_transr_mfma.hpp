@@ -400,13 +400,12 @@ __global__ __launch_bounds__(512) void transr_cons_tile_kernel(RParArgs a, RParB
             const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
             if (a.act[kk]) {
                 slot = (kk * 2 + u) * 2 + role;
-                if (!transr_pair_dup(a, slot)) {
-                    const int i0 = a.si[kk], jj = a.sj[kk];
-                    const int h = a.heads[i0], tt = a.tails[i0];
-                    const int hh = u ? (a.side[kk] ? h : jj) : h;
-                    const int th = u ? (a.side[kk] ? jj : tt) : tt;
-                    ent = role ? th : hh;
-                }
+                const int i0 = a.si[kk], jj = a.sj[kk];
+                const int h = a.heads[i0], tt = a.tails[i0];
+                const int hh = u ? (a.side[kk] ? h : jj) : h;
+                const int th = u ? (a.side[kk] ? jj : tt) : tt;
+                const int e = role ? th : hh;
+                if (!transr_pair_dup(a, slot, r, e)) ent = e;
             }
         } else if (pq < npairs) {
             if (!transr_relpair_dup(a, r)) ent = r;  // entityVec_next_[relation] (transr/trainer.cpp:187)

@@ -63,23 +63,76 @@ struct RParArgs {
     double* loss;        // [B]
     double* proj;        // [B][2][2][ld] compat projections
     int32_t* tile_act;   // [tiles] active updates per tile
-    const int32_t* pprev;  // [B][2][2] this batch's previous slot of the same (relation, entity) (pair_prev_kernel)
-    const int32_t* rlast;  // [nr] this batch's last slot whose entity is the relation id itself
+    // transRNorm pairs are deduplicated per relation per batch (transr_pair_first_kernel)
+    unsigned long long* ptab_keys;  // [mask + 1] stamp | relation | entity; another stamp = empty
+    unsigned long long* ptab_vals;  // stamp << 32 | ~(first active slot)
+    uint32_t ptab_mask, ptab_stamp;
 };
 
-// transRNorm pairs are deduplicated per relation per batch: a slot is skipped
-// when an earlier slot of an active sample holds the same (relation, entity);
-// (entity[r], r) when any active slot of relation r holds entity r.
-__device__ __forceinline__ bool transr_chain_active(const RParArgs& a, int s) {
-    for (; s >= 0; s = a.pprev[s])
-        if (a.act[s >> 2]) return true;
-    return false;
+// The per-batch (relation, entity) -> first active update slot table.  A pair
+// (h', r), (t', r) or (entity[r], r) is the reference's repeated transRNorm
+// call on an already constrained row when an earlier active slot of the batch
+// holds the same (relation, entity) (transr/trainer.cpp:183-188), whichever tile
+// it falls in.  Keys carry the batch stamp, so the table needs no clearing.
+constexpr int kPtabEntBits = 24, kPtabRelBits = 18, kPtabStampBits = 22;
+
+__device__ __forceinline__ unsigned long long ptab_key(const RParArgs& a, int r, int e) {
+    return ((unsigned long long)a.ptab_stamp << (kPtabEntBits + kPtabRelBits)) |
+           ((unsigned long long)r << kPtabEntBits) | (unsigned long long)e;
 }
-__device__ __forceinline__ bool transr_pair_dup(const RParArgs& a, int slot) {
-    return transr_chain_active(a, a.pprev[slot]);
+__device__ __forceinline__ uint32_t ptab_hash(int r, int e) {
+    return ((uint32_t)e * 2654435761u) ^ ((uint32_t)r * 0x9E3779B1u + 0x7F4A7C15u);
+}
+__device__ __forceinline__ bool ptab_current(const RParArgs& a, unsigned long long k) {
+    return (uint32_t)(k >> (kPtabEntBits + kPtabRelBits)) == a.ptab_stamp;
+}
+
+// Records an active slot: the key's table entry keeps the smallest slot.
+__device__ __forceinline__ void ptab_insert(const RParArgs& a, int r, int e, int slot) {
+    const unsigned long long key = ptab_key(a, r, e);
+    uint32_t h = ptab_hash(r, e) & a.ptab_mask;
+    while (true) {
+        unsigned long long k = a.ptab_keys[h];
+        if (k != key && !ptab_current(a, k)) {
+            const unsigned long long old = atomicCAS(a.ptab_keys + h, k, key);
+            k = old == k ? key : old;
+        }
+        if (k == key) break;
+        if (ptab_current(a, k)) h = (h + 1) & a.ptab_mask;  // another key of this batch
+    }
+    atomicMax(a.ptab_vals + h, ((unsigned long long)a.ptab_stamp << 32) | (uint32_t)~(uint32_t)slot);
+}
+
+// The first active slot holding (r, e) this batch, or -1.
+__device__ __forceinline__ int ptab_first(const RParArgs& a, int r, int e) {
+    const unsigned long long key = ptab_key(a, r, e);
+    uint32_t h = ptab_hash(r, e) & a.ptab_mask;
+    while (true) {
+        const unsigned long long k = a.ptab_keys[h];
+        if (k == key) return (int)~(uint32_t)a.ptab_vals[h];
+        if (!ptab_current(a, k)) return -1;
+        h = (h + 1) & a.ptab_mask;
+    }
+}
+
+__device__ __forceinline__ bool transr_pair_dup(const RParArgs& a, int slot, int r, int e) {
+    return ptab_first(a, r, e) < slot;
 }
 __device__ __forceinline__ bool transr_relpair_dup(const RParArgs& a, int r) {
-    return transr_chain_active(a, a.rlast[r]);
+    return ptab_first(a, r, r) >= 0;
+}
+
+// After the batch's hinge decisions: every (h', r), (t', r) slot of an active update.
+static __attribute__((unused)) __global__ __launch_bounds__(256) void transr_pair_first_kernel(RParArgs a) {
+    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= 4 * a.B) return;
+    const int kk = slot >> 2, u = (slot >> 1) & 1, role = slot & 1;
+    if (!a.act[kk]) return;
+    const int i0 = a.si[kk], jj = a.sj[kk];
+    const int h = a.heads[i0], tt = a.tails[i0];
+    const int hh = u ? (a.side[kk] ? h : jj) : h;
+    const int th = u ? (a.side[kk] ? jj : tt) : tt;
+    ptab_insert(a, a.rels[i0], role ? th : hh, slot);
 }
 
 template <typename T>
@@ -548,12 +601,13 @@ __global__ __launch_bounds__(256) void transr_constraint_kernel(RParArgs a, RPar
         if (pq < 4 * cnt) {
             const int q = pq >> 2, u = (pq >> 1) & 1, role = pq & 1;
             const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
-            if (a.act[kk] && !transr_pair_dup(a, (kk * 2 + u) * 2 + role)) {
+            if (a.act[kk]) {
                 const int i0 = a.si[kk], jj = a.sj[kk];
                 const int h = a.heads[i0], tt = a.tails[i0];
                 const int hh = u ? (a.side[kk] ? h : jj) : h;
                 const int th = u ? (a.side[kk] ? jj : tt) : tt;
-                ent = role ? th : hh;
+                const int e = role ? th : hh;
+                if (!transr_pair_dup(a, (kk * 2 + u) * 2 + role, r, e)) ent = e;
             }
         } else if (!transr_relpair_dup(a, r)) {
             ent = r;  // entityVec_next_[relation] (transr/trainer.cpp:187)
@@ -853,6 +907,21 @@ __global__ __launch_bounds__(1024) void rpar_scan_energy_kernel(RParArgs a, RPar
     const int c = blockIdx.x, n = a.n, ld = a.ld;
     const int64_t calls = 2 * (int64_t)a.B;
     const int64_t c0 = (int64_t)c * kScanChunk, c1 = min<int64_t>(calls, c0 + kScanChunk);
+    // the pair-dedupe slots of the chunk's samples (thread 4 q + slot): entity and
+    // relation loaded now, recorded once the hinge is known
+    __shared__ int act_l[kScanChunk / 2];
+    const int nsamp = (int)(c1 - c0) / 2;
+    int pent = -1, prel = -1;
+    if ((int)threadIdx.x < 4 * nsamp) {
+        const int64_t kk = c0 / 2 + (threadIdx.x >> 2);
+        const int u = (threadIdx.x >> 1) & 1, role = threadIdx.x & 1;
+        const int i0 = a.si[kk], jj = a.sj[kk];
+        const int h = a.heads[i0], tt = a.tails[i0];
+        const int hh = u ? (a.side[kk] ? h : jj) : h;
+        const int th = u ? (a.side[kk] ? jj : tt) : tt;
+        pent = role ? th : hh;
+        prel = a.rels[i0];
+    }
     // the sums of all earlier chunks: G thread groups per element, group g over chunks
     // g*16.., (g+G)*16.., sixteen loads in flight (one round trip for FB15k's ~150
     // chunks instead of ten), combined in group order
@@ -912,8 +981,12 @@ __global__ __launch_bounds__(1024) void rpar_scan_energy_kernel(RParArgs a, RPar
         if (l == 0) {
             a.act[kk] = active ? 1 : 0;
             a.loss[kk] = active ? a.margin + ep - en : 0.0;
+            act_l[kk - c0 / 2] = active;
         }
     }
+    __syncthreads();
+    if (pent >= 0 && act_l[threadIdx.x >> 2])
+        ptab_insert(a, prel, pent, (int)(c0 / 2) * 4 + (int)threadIdx.x);
 }
 
 // ---- per-epoch tile index --------------------------------------------------

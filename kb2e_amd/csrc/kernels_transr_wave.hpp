@@ -142,6 +142,9 @@ __global__ __launch_bounds__(128) void transr_proj_wave_kernel(RParArgs a, RParB
             a.act[kk] = active ? 1 : 0;
             a.loss[kk] = active ? a.margin + (double)ep - (double)er : 0.0;
         }
+        // every row of an active sample records its (entity, r) slot for the pair dedupe
+        const T en3 = quad_bcast<3>(er);
+        if (has && kq == 0 && (double)ep + a.margin > (double)en3) ptab_insert(a, r, e, kk * 4 + which);
     }
     // y = W0 x (transr/trainer.cpp:168-169): Y^T = W0 X^T, the t / t' columns
     T* yrow = bf.y + ((int64_t)kk * 2 + u) * ld;
@@ -237,7 +240,8 @@ __global__ __launch_bounds__(256) void transr_grad_wave_kernel(RParArgs a, RParB
             const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
             if (a.act[kk]) {
                 slot = (kk * 2 + u) * 2 + role;
-                if (!transr_pair_dup(a, slot)) ent = bf.trow[blockIdx.x * kTRows + pq];
+                const int e = bf.trow[blockIdx.x * kTRows + pq];
+                if (!transr_pair_dup(a, slot, r, e)) ent = e;
             }
         } else if (pq == 4 * cnt && relpair && !transr_relpair_dup(a, r)) {
             ent = r;  // entityVec_next_[relation] (transr/trainer.cpp:187)

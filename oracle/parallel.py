@@ -149,8 +149,9 @@ def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, 
 
     Per relation of the batch: pairs (h', r), (t', r) of the active updates in
     (sample, update, role) order, then (entity'[r], r) (transr/trainer.cpp:187);
-    first occurrences per relation only (pair_prev_kernel, transr_pair_dup:
-    independent of how the GPU cuts the relation into tiles, so St is unused);
+    first occurrences per relation only (the GPU's per-batch (relation, entity)
+    table, kernels_transr_parallel.hpp transr_pair_dup: independent of how the
+    relation is cut into tiles, so St is unused);
     the loop in Jacobi form to first order, iterated on the projection
     p = W^T a: p <- p - 2 lr W^T W p - 2 lr |a0|^2 p, G += 2 p while |p|^2 > 1,
     then da = -lr W G, dW = -lr a0 G^T (kernels_transr_mfma.hpp).

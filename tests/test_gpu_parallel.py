@@ -139,6 +139,24 @@ def test_transr_parallel_compat(dim, St, mfma, monkeypatch):
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=True, mfma=mfma)
 
 
+def _hub_dataset(ne=300, nr=6, count=4000, seed=5):
+    """Entity 0 heads ~half the triples: its event segments run to hundreds of
+    events a batch (pair_prev_long_kernel's LDS table path)."""
+    rng = np.random.default_rng(seed)
+    h = np.where(rng.random(count) < 0.5, 0, rng.integers(1, ne, count))
+    t = rng.integers(1, ne, count)
+    r = rng.integers(0, nr, count)
+    tr = np.unique(np.stack([h, t, r], 1).astype(np.int32), axis=0)
+    tr = tr[rng.permutation(len(tr))]
+    return data.Dataset(ne, nr, tr, tr[:0], tr[:0])
+
+
+@pytest.mark.parametrize("St", [8, 1])
+def test_transr_parallel_hub_entity(St, monkeypatch):
+    """Per-relation pair dedupe through long entity segments (hub entity)."""
+    _transr_vs_model(_hub_dataset(), 20, 2, monkeypatch, St=St, batches=5)
+
+
 def test_transr_parallel_independent_of_tile_size(monkeypatch):
     """transRNorm pairs are deduplicated per relation per batch, so cutting the
     relations into tiles of 1, 2 or 8 samples changes only the order of the
