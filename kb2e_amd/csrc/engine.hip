@@ -70,7 +70,7 @@ void check_dataflow(kb2e_ctx* c);
 void build_owner_index(kb2e_ctx* c);
 void prepare_relowner_kernels();
 void setup_transr_parallel(kb2e_ctx* c);
-void build_transr_tiles(kb2e_ctx* c, bool tiles, hipStream_t st);
+void build_transr_tiles(kb2e_ctx* c, bool tiles, hipStream_t st, int set);
 template <typename T>
 void run_batch_transr_parallel(kb2e_ctx* c, int64_t b);
 template <typename T, int CH>
@@ -161,6 +161,8 @@ struct kb2e_ctx {
     DevBuf rpar_y, rpar_wpart, rpar_rpart, rpar_tile_act, rpar_pair, rpar_relpair, rpar_relpair_stamp, rpar_tiles,
         rpar_ntiles, rpar_tile_first, rpar_rel_begin, rpar_scan;
     DevBuf rpar_ptab_keys, rpar_ptab_vals;  // transRNorm pair dedupe: per-batch (relation, entity) table
+    DevBuf rpar_batch_t0, rpar_td_r, rpar_td_cnt, rpar_td_kk, rpar_td_ent;  // per-epoch tile descriptors
+    DevBuf sh_rpar_batch_t0, sh_rpar_td_r, sh_rpar_td_cnt, sh_rpar_td_kk, sh_rpar_td_ent;
     hipStream_t fold_stream = nullptr;  // the long-segment fold runs beside the per-row fold
     hipEvent_t ev_fold_a = nullptr, ev_fold_b = nullptr;
     DevBuf long_list, long_count;
@@ -380,6 +382,9 @@ std::vector<std::pair<DevBuf*, DevBuf*>> index_bufs(kb2e_ctx* c) {
             {&c->ev_slot_sorted, &c->sh_ev_slot_sorted}, {&c->ev_inv, &c->sh_ev_inv}, {&c->seg_row, &c->sh_seg_row},
             {&c->rpar_ntiles, &c->sh_rpar_ntiles}, {&c->rpar_rel_begin, &c->sh_rpar_rel_begin},
             {&c->rpar_tile_first, &c->sh_rpar_tile_first}, {&c->rpar_tiles, &c->sh_rpar_tiles},
+            {&c->rpar_batch_t0, &c->sh_rpar_batch_t0}, {&c->rpar_td_r, &c->sh_rpar_td_r},
+            {&c->rpar_td_cnt, &c->sh_rpar_td_cnt}, {&c->rpar_td_kk, &c->sh_rpar_td_kk},
+            {&c->rpar_td_ent, &c->sh_rpar_td_ent},
 
             {&c->par_long_list, &c->sh_par_long_list}, {&c->par_long_count, &c->sh_par_long_count}};
 }
@@ -460,7 +465,7 @@ void build_index(kb2e_ctx* c, hipStream_t st, int set) {
             seg_rows_kernel<<<256, 256, 0, st>>>(c->keys_sorted.as<uint64_t>(), c->seg_start.as<int32_t>(),
                                                        c->nseg.as<int32_t>(), c->kl, c->seg_row.as<int32_t>());
             HIPCHK(hipGetLastError());
-            if (c->cfg.model != KB2E_TRANSE) build_transr_tiles(c, c->cfg.model == KB2E_TRANSR, st);
+            if (c->cfg.model != KB2E_TRANSE) build_transr_tiles(c, c->cfg.model == KB2E_TRANSR, st, set);
         }
         if (c->cfg.model != KB2E_TRANSR && c->cfg.schedule == KB2E_SCHEDULE_PARALLEL && c->apply_long_min > 0) {
             long_lists_kernel<<<(int)c->nb, 1024, 0, st>>>(

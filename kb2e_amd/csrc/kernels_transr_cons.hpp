@@ -205,13 +205,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
     constexpr int KN = sizeof(T) == 8 ? 4 * KS : NP;
     constexpr int kOut = (NB * NB + kConsWaves - 1) / kConsWaves;  // K output tiles per wave
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tb = a.tile_first[a.batch_seg[a.batch]];
-    const int t = tb + blockIdx.x;
-    if (t >= a.tile_first[a.batch_seg[a.batch + 1]]) return;
-    int r, e0, cnt;
-    tile_range(a, t, r, e0, cnt);
-    (void)e0;
-    (void)cnt;
+    const int t = a.batch_t0[a.batch] + blockIdx.x;
+    if (t >= a.batch_t0[a.batch + 1]) return;
+    const int r = a.td_r[t];
     const int n = a.n, ld = a.ld;
     const int w = threadIdx.x >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
     T* Wl = (T*)smem;

@@ -67,6 +67,13 @@ struct RParArgs {
     unsigned long long* ptab_keys;  // [mask + 1] stamp | relation | entity; another stamp = empty
     unsigned long long* ptab_vals;  // stamp << 32 | ~(first active slot)
     uint32_t ptab_mask, ptab_stamp;
+    // per-epoch tile descriptors (rtile_desc_kernel; matrix-core wave kernels): the
+    // tiles' relation, sample count, samples and rows without the index chain
+    const int32_t* batch_t0;  // [nb + 1] first tile of each batch
+    const int32_t* td_r;      // [tiles]
+    const int32_t* td_cnt;    // [tiles]
+    const int32_t* td_kk;     // [tiles][8] batch-local sample of tile sample q
+    const int32_t* td_ent;    // [tiles][8][4] entity of row (q, h / t / h' / t'), -1 past cnt
 };
 
 // The per-batch (relation, entity) -> first active update slot table.  A pair
@@ -1021,6 +1028,61 @@ static __attribute__((unused)) __global__ __launch_bounds__(256) void rtile_scat
     const int nseg = *nseg_p;
     for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x)
         for (int q = 0; q < ntiles[s]; ++q) tiles[tile_first[s] + q] = RTile{s, q};
+}
+
+// Per epoch, after the tiles: each tile's relation, count, samples and the
+// entities of its rows (sample q: h, t, h', t'), and the first tile of each batch.
+struct RTileDescArgs {
+    const uint64_t* keys;
+    const int32_t* seg_start;
+    const int32_t* seg_row;
+    const RTile* tiles;
+    const int32_t* tile_first;
+    const int32_t* nseg;
+    const int32_t* batch_seg;
+    int32_t nb, St, ne, B;
+    KeyLayout kl;
+    const int32_t* si;  // the epoch's sample stream
+    const int32_t* sj;
+    const uint8_t* side;
+    const int32_t* heads;
+    const int32_t* tails;
+    int32_t* batch_t0;
+    int32_t* td_r;
+    int32_t* td_cnt;
+    int32_t* td_kk;
+    int32_t* td_ent;
+};
+
+static __attribute__((unused)) __global__ __launch_bounds__(256) void rtile_desc_kernel(RTileDescArgs a) {
+    const int ntiles = a.tile_first[*a.nseg];
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid <= a.nb) a.batch_t0[gid] = a.tile_first[a.batch_seg[gid]];
+    for (int64_t x = gid; x < (int64_t)ntiles * 8; x += (int64_t)gridDim.x * blockDim.x) {
+        const int t = (int)(x >> 3), q = (int)(x & 7);
+        const RTile tl = a.tiles[t];
+        const int p0 = a.seg_start[tl.seg], p1 = a.seg_start[tl.seg + 1];
+        const int f = tl.q * a.St, cnt = min(a.St, (p1 - p0) / 2 - f);
+        if (q == 0) {
+            a.td_r[t] = a.seg_row[tl.seg] - a.ne;
+            a.td_cnt[t] = cnt;
+        }
+        int kk = 0, e4[4] = {-1, -1, -1, -1};
+        if (q < cnt) {
+            const uint64_t key = a.keys[p0 + 2 * (f + q)];
+            kk = a.kl.kk_of(key);
+            const int64_t k = (int64_t)a.kl.batch_of(key) * a.B + kk;
+            const int i0 = a.si[k], jj = a.sj[k];
+            const int h = a.heads[i0], tt = a.tails[i0];
+            const bool sd = a.side[k] != 0;
+            e4[0] = h;
+            e4[1] = tt;
+            e4[2] = sd ? h : jj;
+            e4[3] = sd ? jj : tt;
+        }
+        a.td_kk[x] = kk;
+        *(int4*)(a.td_ent + 4 * x) = make_int4(e4[0], e4[1], e4[2], e4[3]);
+    }
 }
 
 }  // namespace kb2e

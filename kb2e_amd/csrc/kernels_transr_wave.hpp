@@ -47,23 +47,19 @@ __global__ __launch_bounds__(128) void transr_proj_wave_kernel(RParArgs a, RParB
     using M = Mfma16<T>;
     constexpr int NB = (KS + 3) / 4, NP = 16 * NB, L = NP + 2, NS = NP / 4;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int t = a.tile_first[a.batch_seg[a.batch]] + blockIdx.x;
-    if (t >= a.tile_first[a.batch_seg[a.batch + 1]]) return;
-    int r, e0, cnt;
-    tile_range(a, t, r, e0, cnt);
+    // the tile from the per-epoch descriptors: two dependent loads to the rows
+    const int t = a.batch_t0[a.batch] + blockIdx.x;
+    if (t >= a.batch_t0[a.batch + 1]) return;
+    const int r = a.td_r[t], cnt = a.td_cnt[t];
     const int n = a.n, ld = a.ld;
     const int w = threadIdx.x >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
     T* Wl = (T*)smem;
     // this lane's row: sample q, role which (0 h, 1 t, 2 h', 3 t')
     const int q = w * 4 + (l16 >> 2), which = l16 & 3;
     const bool has = q < cnt;
-    const uint64_t key = a.keys[e0 + 2 * (has ? q : 0)];
-    const int kk = a.kl.kk_of(key);
-    const int i0 = a.si[kk], jj = a.sj[kk];
-    const int h = a.heads[i0], tt = a.tails[i0];
-    const bool sd = a.side[kk] != 0;
-    const int e = which == 0 ? h : which == 1 ? tt : which == 2 ? (sd ? h : jj) : (sd ? jj : tt);
-    if (kq == 0) bf.trow[blockIdx.x * kTRows + w * 16 + l16] = has ? e : -1;  // for the transRNorm pairs
+    const int kk = a.td_kk[t * 8 + q];
+    const int ed = a.td_ent[(t * 8 + q) * 4 + which];
+    const int e = ed < 0 ? 0 : ed;
     {  // W0 as element pairs, every load in flight before the LDS stores
         using T2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
         constexpr int kPairs = NP * L / 2, kThreads = kProjWaves * kWave;
@@ -167,21 +163,20 @@ __global__ __launch_bounds__(256) void transr_grad_wave_kernel(RParArgs a, RParB
     constexpr int NB = (KS + 3) / 4;
     constexpr int kOut = (NB * NB + kConsWaves - 1) / kConsWaves;  // output tiles per wave
     constexpr int kSteps = 4;  // 2 St <= 16 updates (St <= 8 on the matrix-core path)
-    const int t = a.tile_first[a.batch_seg[a.batch]] + blockIdx.x;
-    if (t >= a.tile_first[a.batch_seg[a.batch + 1]]) return;
-    int r, e0, cnt;
-    tile_range(a, t, r, e0, cnt);
+    const int t = a.batch_t0[a.batch] + blockIdx.x;
+    if (t >= a.batch_t0[a.batch + 1]) return;
+    const int r = a.td_r[t], cnt = a.td_cnt[t];
     const int n = a.n, ld = a.ld;
     const int w = threadIdx.x >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
     const int nu = 2 * cnt;
-    // this lane's update of every k-step (u = 4 s + l / 16): export row and coefficient
+    // this lane's update of every k-step (u = 4 s + l / 16: sample u / 2, update u & 1):
+    // export row and coefficient
     int rowu[kSteps];
     T cu[kSteps];
 #pragma unroll
     for (int s = 0; s < kSteps; ++s) {
         const int u = 4 * s + kq;
-        const uint64_t key = a.keys[e0 + (u < nu ? u : 0)];
-        const int kk = a.kl.kk_of(key), side = (int)((key >> 3) & 1);
+        const int kk = a.td_kk[t * 8 + (u >> 1)], side = u & 1;
         rowu[s] = kk * 2 + side;
         cu[s] = (u < nu && a.act[kk]) ? (T)(-(side ? 1.0 : -1.0) * a.lr) : T(0);
     }
@@ -215,7 +210,7 @@ __global__ __launch_bounds__(256) void transr_grad_wave_kernel(RParArgs a, RParB
     }
     if (threadIdx.x == 0) {  // the tile's active updates
         int nact = 0;
-        for (int u = 0; u < nu; ++u) nact += a.act[a.kl.kk_of(a.keys[e0 + u])] != 0;
+        for (int u = 0; u < nu; ++u) nact += a.act[a.td_kk[t * 8 + (u >> 1)]] != 0;
         a.tile_act[t] = nact;
     }
     if (w == kConsWaves - 1) {
@@ -237,10 +232,10 @@ __global__ __launch_bounds__(256) void transr_grad_wave_kernel(RParArgs a, RParB
         int ent = -1, slot = -1;
         if (pq < 4 * cnt) {
             const int q = pq >> 2, u = (pq >> 1) & 1, role = pq & 1;
-            const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
+            const int kk = a.td_kk[t * 8 + q];
             if (a.act[kk]) {
                 slot = (kk * 2 + u) * 2 + role;
-                const int e = bf.trow[blockIdx.x * kTRows + pq];
+                const int e = a.td_ent[t * 32 + pq];
                 if (!transr_pair_dup(a, slot, r, e)) ent = e;
             }
         } else if (pq == 4 * cnt && relpair && !transr_relpair_dup(a, r)) {
