@@ -157,7 +157,7 @@ struct kb2e_ctx {
     bool rpar_mfma = false;  // matrix-core tile kernels (kernels_transr_mfma.hpp)
     bool rpar_cons_wave = false;  // transRNorm rounds in one wave's registers (kernels_transr_cons.hpp)
     size_t rpar_cons_lds = 0;
-    DevBuf rpar_pflag, rpar_cons_tile, rpar_trow, rpar_cpairs, rpar_cnrows;
+    DevBuf rpar_pflag, rpar_cons_tile, rpar_cpairs, rpar_cnrows;
     DevBuf rpar_y, rpar_wpart, rpar_rpart, rpar_tile_act, rpar_pair, rpar_relpair, rpar_relpair_stamp, rpar_tiles,
         rpar_ntiles, rpar_tile_first, rpar_rel_begin, rpar_scan;
     DevBuf rpar_ptab_keys, rpar_ptab_vals;  // transRNorm pair dedupe: per-batch (relation, entity) table

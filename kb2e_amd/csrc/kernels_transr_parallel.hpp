@@ -163,7 +163,6 @@ struct RParBufs {
     // register-fragment kernels (kernels_transr_wave.hpp): phase A's entity of every
     // (tile, V row) and the transRNorm pairs of every tile, compacted by the gradient
     // kernel: [tile][kCPairs] entities then [tile][kCPairs] slots, and the row count
-    int32_t* trow;       // [tiles][32]
     int32_t* cpairs;     // [tiles][2][kCPairs]
     int32_t* cnrows;     // [tiles]
     int32_t stats;       // count transRNorm rounds (tools)
@@ -171,7 +170,6 @@ struct RParBufs {
 };
 
 __host__ __device__ constexpr int rm_up16_host_dev(int v) { return (v + 15) & ~15; }
-constexpr int kTRows = 32;   // V rows of a tile on the register-fragment path (4 St, St <= 8)
 constexpr int kCPairs = 64;  // transRNorm pairs of a tile (4 St + 1 <= 64)
 
 template <typename T>
