@@ -190,17 +190,18 @@ __global__ __launch_bounds__(1024) void long_lists_kernel(const int32_t* seg_sta
 // last share of them.
 constexpr int kApplyWaves = 16;
 
+// (the body takes its workgroup index and count: TransH runs it in one launch
+// with the relation-normal sums, transh_phase_b_kernel; arguments by value)
 template <typename T, int CH, bool L1>
-__global__ __launch_bounds__(1024) void transe_apply_kernel(FoldArgs<T> a, EventRecs er, const int32_t* long_list,
-                                                            const int32_t* long_count, int32_t cap) {
+__device__ __forceinline__ void transe_apply_body(FoldArgs<T> a, EventRecs er, const int32_t* long_list,
+                                                  const int32_t* long_count, int32_t cap, int bid, int G) {
     using A = typename DeltaAcc<T, CH, L1>::A;
     __shared__ A part[kApplyWaves][CH * kVec][kWave];
     __shared__ int dirty_any;
     const int w = threadIdx.x >> 6, l = lane_id();
     const int nlong = a.long_min > 0 ? long_count[a.batch] : 0;
     const int32_t* list = long_list + (int64_t)a.batch * cap;
-    const int G = gridDim.x;
-    for (int q = blockIdx.x; q < nlong; q += G) {
+    for (int q = bid; q < nlong; q += G) {
         const int s = list[q];
         const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
         T* ptr = row_ptr(a, er.seg_row[s]);
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(1024) void transe_apply_kernel(FoldArgs<T> a, Event
         __syncthreads();
     }
     const int s0 = a.batch_seg[a.batch], s1 = a.batch_seg[a.batch + 1];
-    const int rot = (blockIdx.x + G - (nlong % G)) % G;
+    const int rot = (bid + G - (nlong % G)) % G;
     const int wave = rot * kApplyWaves + w;
     for (int s = s0 + wave; s < s1; s += G * kApplyWaves) {
         const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
@@ -245,6 +246,12 @@ __global__ __launch_bounds__(1024) void transe_apply_kernel(FoldArgs<T> a, Event
         accumulate_segment<T, CH, L1>(a, er, p0, p1, 0, 1, acc);
         apply_row<T, CH, L1>(a, ptr, V, acc);
     }
+}
+
+template <typename T, int CH, bool L1>
+__global__ __launch_bounds__(1024) void transe_apply_kernel(FoldArgs<T> a, EventRecs er, const int32_t* long_list,
+                                                            const int32_t* long_count, int32_t cap) {
+    transe_apply_body<T, CH, L1>(a, er, long_list, long_count, cap, blockIdx.x, gridDim.x);
 }
 
 }  // namespace kb2e

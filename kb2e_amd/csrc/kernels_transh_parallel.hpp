@@ -52,10 +52,10 @@ struct HParArgs {
 // hottest relation (~1100 events on FB15k-shaped batches) sets the time, so
 // the default is 16 waves (8 and 4 measured 16% and 50% slower).
 template <typename T, int CH, int NWV>
-__global__ __launch_bounds__(NWV * kWave) void transh_w_apply_kernel(HParArgs<T> a) {
+__device__ __forceinline__ void transh_w_apply_body(HParArgs<T> a, int bid) {
     __shared__ T part[NWV][CH * kVec][kWave];
     __shared__ int any;
-    const int s = a.rel_begin[a.batch] + blockIdx.x;
+    const int s = a.rel_begin[a.batch] + bid;
     if (s >= a.batch_seg[a.batch + 1]) return;
     const int w = threadIdx.x >> 6, l = lane_id();
     const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
@@ -126,6 +126,22 @@ __global__ __launch_bounds__(NWV * kWave) void transh_w_apply_kernel(HParArgs<T>
         }
     W.norm(a.n, false);
     W.store(wrow, a.n);
+}
+
+template <typename T, int CH, int NWV>
+__global__ __launch_bounds__(NWV * kWave) void transh_w_apply_kernel(HParArgs<T> a) {
+    transh_w_apply_body<T, CH, NWV>(a, blockIdx.x);
+}
+
+// Phase B's two sums in one launch (they touch disjoint tables): workgroups
+// [0, wgrid) the relation normals, the rest the TransE apply of the h/t/r rows,
+// so the hottest relation's normal overlaps the row sums instead of preceding them.
+template <typename T, int CH>
+__global__ __launch_bounds__(1024) void transh_phase_b_kernel(HParArgs<T> h, FoldArgs<T> fa, EventRecs er,
+                                                             const int32_t* long_list, const int32_t* long_count,
+                                                             int32_t cap, int32_t wgrid) {
+    if ((int)blockIdx.x < wgrid) transh_w_apply_body<T, CH, 16>(h, blockIdx.x);
+    else transe_apply_body<T, CH, true>(fa, er, long_list, long_count, cap, blockIdx.x - wgrid, gridDim.x - wgrid);
 }
 
 // One wave per active sample: w'.a for the rows r', h', t' of both updates
