@@ -124,3 +124,36 @@ def test_transr_parallel_first_order_equals_reference(distance):
         d_ref = np.abs(ref - start).max()
         assert d_ref > 0
         assert np.abs((got - start) - (ref - start)).max() <= 1e-3 * d_ref
+
+
+def test_transr_constraint_pairs_once_per_relation():
+    """transRNorm pairs of the PARALLEL schedule: each (relation, entity) of the
+    batch's active updates is constrained once, whatever the tiling (St), and
+    (entity[r], r) is skipped when an update of r already holds entity r."""
+    from oracle.parallel import transr_constraint
+
+    rng = np.random.default_rng(4)
+    n, rate = 4, 0.01
+    ent0 = rng.standard_normal((5, n))
+    ent0 *= 1.5 / np.linalg.norm(ent0, axis=1, keepdims=True)  # |W^T a| > 1 with W = I: every pair violates
+    W0 = np.stack([np.eye(n), np.eye(n)])
+    h, t = np.array([0, 0]), np.array([1, 2])
+    nh, nt = np.array([0, 3]), np.array([4, 2])
+    r, act = np.array([0, 0]), np.array([True, True])
+
+    def single(a0, Wm):  # one pair, as transr_constraint's loop
+        G, s0, p = np.zeros(n), a0 @ a0, Wm.T @ a0
+        while p @ p > 1.0:
+            G += 2.0 * p
+            p = p - 2.0 * rate * (Wm.T @ (Wm @ p)) - 2.0 * rate * s0 * p
+        return -rate * (Wm @ G), np.outer(-rate * a0, G)
+
+    want_e, want_w = ent0.copy(), W0.copy()
+    for e in (0, 1, 4, 2, 3):  # first occurrences in (sample, update, role) order; entity 0 = relation 0's pair
+        da, dw = single(ent0[e], W0[0])
+        want_e[e] += da
+        want_w[0] += dw
+    for St in (1, 2, 8):
+        ent, W = ent0.copy(), W0.copy()
+        transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St)
+        assert np.abs(ent - want_e).max() < 1e-15 and np.abs(W - want_w).max() < 1e-15
