@@ -371,11 +371,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
             }
         lv = lv && row4_sum(nr) > T(1);
     }
-    // pair records da = -lr W0 G  (da^T = W0 G^T, G^T the B operand)
+    // pair records da = -lr W0 G
+    const uint32_t v16 = (uint32_t)__ballot(vio0) & 0xFFFFu;
+    const bool valu_rec = __builtin_popcount(v16) <= kValuRows;
+    if (valu_rec && !(bf.dbg & 4)) {
+        // few violating rows (the usual case): on the VALU, one row at a time, lane j
+        // element j: da_j = W0[j] . G, G through this wave's SP rows
+        int rv[kValuRows];
+        uint32_t mm = v16;
+#pragma unroll
+        for (int j = 0; j < kValuRows; ++j) {
+            rv[j] = mm ? (int)__builtin_ctz(mm) : -1;
+            mm &= mm - 1;
+        }
+#pragma unroll
+        for (int j = 0; j < kValuRows; ++j)
+            if (l16 == rv[j])
+#pragma unroll
+                for (int s = 0; s < NS; ++s) SP[j * NP + kmap<T>(s, kq)] = gs[s];
+        wave_lds_sync();
+        const T* Wj = Wl + (l < n ? l : 0) * L;
+#pragma unroll 1
+        for (int j = 0; j < kValuRows; ++j) {
+            if (rv[j] < 0) break;
+            const int slj = readlane_i32(sl, rv[j]);
+            T acc[4] = {T(0), T(0), T(0), T(0)};
+#pragma unroll
+            for (int k = 0; k < KN; ++k) acc[k & 3] = fma(Wj[k], SP[j * NP + k], acc[k & 3]);
+            T* dj = slj >= 0 ? bf.pair + (int64_t)slj * ld : bf.relpair + (int64_t)r * ld;
+            if (l < n) dj[l] = -lr * ((acc[0] + acc[1]) + (acc[2] + acc[3]));
+            if (slj == -2 && l == 0) bf.relpair_stamp[r] = bf.stamp;
+        }
+        wave_lds_sync();
+    }
+    // (da^T = W0 G^T, G^T the B operand)
     T* dst = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
 #pragma unroll
     for (int jb = 0; jb < NB; ++jb) {
-        if (bf.dbg & 4) break;
+        if ((bf.dbg & 4) || valu_rec) break;
         typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
 #pragma unroll
         for (int s = 0; s < KS; ++s) acc = M::mma(Wl[(jb * 16 + l16) * L + kmap<T>(s, kq)], gs[s], acc);
@@ -385,7 +418,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
             if (vio0 && j < n) dst[j] = -lr * acc[q];
         }
     }
-    if (vio0 && sl == -2) bf.relpair_stamp[r] = bf.stamp;
+    if (vio0 && sl == -2 && !valu_rec) bf.relpair_stamp[r] = bf.stamp;
     }  // vm16
     const unsigned long long ck2 = bf.stats ? clock64() : ck2r;
     // the tile's matrix partial dW[j][i] = sum_p (-lr a0[p][j]) G[p][i]: the
