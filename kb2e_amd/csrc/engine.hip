@@ -160,7 +160,7 @@ struct kb2e_ctx {
     DevBuf rpar_pflag, rpar_cons_tile, rpar_cpairs, rpar_cnrows;
     DevBuf rpar_y, rpar_wpart, rpar_rpart, rpar_tile_act, rpar_pair, rpar_relpair, rpar_relpair_stamp, rpar_tiles,
         rpar_ntiles, rpar_tile_first, rpar_rel_begin, rpar_scan;
-    DevBuf rpar_ptab_keys, rpar_ptab_vals;  // transRNorm pair dedupe: per-batch (relation, entity) table
+    DevBuf rpar_ptab;  // transRNorm pair dedupe: two per-batch (relation, entity) tables
     DevBuf rpar_batch_t0, rpar_td_r, rpar_td_cnt, rpar_td_kk, rpar_td_ent;  // per-epoch tile descriptors
     DevBuf sh_rpar_batch_t0, sh_rpar_td_r, sh_rpar_td_cnt, sh_rpar_td_kk, sh_rpar_td_ent;
     hipStream_t fold_stream = nullptr;  // the long-segment fold runs beside the per-row fold

@@ -63,10 +63,10 @@ struct RParArgs {
     double* loss;        // [B]
     double* proj;        // [B][2][2][ld] compat projections
     int32_t* tile_act;   // [tiles] active updates per tile
-    // transRNorm pairs are deduplicated per relation per batch (transr_pair_first_kernel)
-    unsigned long long* ptab_keys;  // [mask + 1] stamp | relation | entity; another stamp = empty
-    unsigned long long* ptab_vals;  // stamp << 32 | ~(first active slot)
-    uint32_t ptab_mask, ptab_stamp;
+    // transRNorm pairs are deduplicated per relation per batch (ptab_insert / transr_pair_dup)
+    unsigned long long* ptab;       // [mask + 1] this batch's table: (relation, entity) << 22 | first active slot
+    unsigned long long* ptab_next;  // the other one (the next batch's): cleared by the inserting kernel
+    uint32_t ptab_mask;
     // per-epoch tile descriptors (rtile_desc_kernel; matrix-core wave kernels): the
     // tiles' relation, sample count, samples and rows without the index chain
     const int32_t* batch_t0;  // [nb + 1] first tile of each batch
@@ -80,46 +80,51 @@ struct RParArgs {
 // (h', r), (t', r) or (entity[r], r) is the reference's repeated transRNorm
 // call on an already constrained row when an earlier active slot of the batch
 // holds the same (relation, entity) (transr/trainer.cpp:183-188), whichever tile
-// it falls in.  Keys carry the batch stamp, so the table needs no clearing.
-constexpr int kPtabEntBits = 24, kPtabRelBits = 18, kPtabStampBits = 22;
+// it falls in.  One word per entry, all ones = empty; two tables alternate by
+// batch, the inserting kernel of batch b clearing batch b + 1's (whose last
+// reader was batch b - 1's transRNorm step).
+constexpr int kPtabEntBits = 24, kPtabRelBits = 18, kPtabSlotBits = 22;
+constexpr unsigned long long kPtabEmpty = ~0ull;
 
-__device__ __forceinline__ unsigned long long ptab_key(const RParArgs& a, int r, int e) {
-    return ((unsigned long long)a.ptab_stamp << (kPtabEntBits + kPtabRelBits)) |
-           ((unsigned long long)r << kPtabEntBits) | (unsigned long long)e;
+__device__ __forceinline__ unsigned long long ptab_key(int r, int e) {
+    return ((unsigned long long)r << kPtabEntBits) | (unsigned long long)e;
 }
 __device__ __forceinline__ uint32_t ptab_hash(int r, int e) {
     return ((uint32_t)e * 2654435761u) ^ ((uint32_t)r * 0x9E3779B1u + 0x7F4A7C15u);
 }
-__device__ __forceinline__ bool ptab_current(const RParArgs& a, unsigned long long k) {
-    return (uint32_t)(k >> (kPtabEntBits + kPtabRelBits)) == a.ptab_stamp;
-}
 
-// Records an active slot: the key's table entry keeps the smallest slot.
+// Records an active slot: the key's entry keeps the smallest slot (one CAS when
+// the key is new, an atomicMin when it is already there).
 __device__ __forceinline__ void ptab_insert(const RParArgs& a, int r, int e, int slot) {
-    const unsigned long long key = ptab_key(a, r, e);
+    const unsigned long long key = ptab_key(r, e);
+    const unsigned long long word = (key << kPtabSlotBits) | (unsigned long long)slot;
     uint32_t h = ptab_hash(r, e) & a.ptab_mask;
     while (true) {
-        unsigned long long k = a.ptab_keys[h];
-        if (k != key && !ptab_current(a, k)) {
-            const unsigned long long old = atomicCAS(a.ptab_keys + h, k, key);
-            k = old == k ? key : old;
+        const unsigned long long old = atomicCAS(a.ptab + h, kPtabEmpty, word);
+        if (old == kPtabEmpty) return;
+        if ((old >> kPtabSlotBits) == key) {
+            atomicMin(a.ptab + h, word);
+            return;
         }
-        if (k == key) break;
-        if (ptab_current(a, k)) h = (h + 1) & a.ptab_mask;  // another key of this batch
+        h = (h + 1) & a.ptab_mask;
     }
-    atomicMax(a.ptab_vals + h, ((unsigned long long)a.ptab_stamp << 32) | (uint32_t)~(uint32_t)slot);
 }
 
 // The first active slot holding (r, e) this batch, or -1.
 __device__ __forceinline__ int ptab_first(const RParArgs& a, int r, int e) {
-    const unsigned long long key = ptab_key(a, r, e);
+    const unsigned long long key = ptab_key(r, e);
     uint32_t h = ptab_hash(r, e) & a.ptab_mask;
     while (true) {
-        const unsigned long long k = a.ptab_keys[h];
-        if (k == key) return (int)~(uint32_t)a.ptab_vals[h];
-        if (!ptab_current(a, k)) return -1;
+        const unsigned long long w = a.ptab[h];
+        if (w == kPtabEmpty) return -1;
+        if ((w >> kPtabSlotBits) == key) return (int)(w & ((1ull << kPtabSlotBits) - 1));
         h = (h + 1) & a.ptab_mask;
     }
+}
+
+// The next batch's table, cleared by the threads of the inserting kernel.
+__device__ __forceinline__ void ptab_clear_next(const RParArgs& a, int64_t tid, int64_t nthreads) {
+    for (int64_t q = tid; q <= (int64_t)a.ptab_mask; q += nthreads) a.ptab_next[q] = kPtabEmpty;
 }
 
 __device__ __forceinline__ bool transr_pair_dup(const RParArgs& a, int slot, int r, int e) {
@@ -132,6 +137,7 @@ __device__ __forceinline__ bool transr_relpair_dup(const RParArgs& a, int r) {
 // After the batch's hinge decisions: every (h', r), (t', r) slot of an active update.
 static __attribute__((unused)) __global__ __launch_bounds__(256) void transr_pair_first_kernel(RParArgs a) {
     const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    ptab_clear_next(a, slot, (int64_t)gridDim.x * blockDim.x);
     if (slot >= 4 * a.B) return;
     const int kk = slot >> 2, u = (slot >> 1) & 1, role = slot & 1;
     if (!a.act[kk]) return;
@@ -989,6 +995,7 @@ __global__ __launch_bounds__(1024) void rpar_scan_energy_kernel(RParArgs a, RPar
             act_l[kk - c0 / 2] = active;
         }
     }
+    ptab_clear_next(a, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
     __syncthreads();
     if (pent >= 0 && act_l[threadIdx.x >> 2])
         ptab_insert(a, prel, pent, (int)(c0 / 2) * 4 + (int)threadIdx.x);

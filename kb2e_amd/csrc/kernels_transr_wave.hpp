@@ -47,6 +47,9 @@ __global__ __launch_bounds__(128) void transr_proj_wave_kernel(RParArgs a, RParB
     using M = Mfma16<T>;
     constexpr int NB = (KS + 3) / 4, NP = 16 * NB, L = NP + 2, NS = NP / 4;
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    // fixed energy: this kernel fills the pair-dedupe table (every thread of the grid
+    // clears its share of the next batch's first)
+    if (!a.compat) ptab_clear_next(a, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
     // the tile from the per-epoch descriptors: two dependent loads to the rows
     const int t = a.batch_t0[a.batch] + blockIdx.x;
     if (t >= a.batch_t0[a.batch + 1]) return;
