@@ -432,7 +432,8 @@ void build_index(kb2e_ctx* c, hipStream_t st, int set) {
         // full-key order (sentinels stay last: batch nb-1 is never all-ones).
         const int lo_bit = getenv("KB2E_SORT_FULLKEY") ? 0 : c->kl.row_shift();
         size_t tb = c->sort_tmp_bytes;
-        if (c->parallel()) {  // the sorted position of every emitted key, for phase A's event records
+        if (c->parallel() && c->cfg.model != KB2E_TRANSR) {  // the sorted position of every emitted key, for
+                                                              // phase A's event records (TransE / TransH)
             HIPCHK(hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tb, c->keys.as<uint64_t>(),
                                                       c->keys_sorted.as<uint64_t>(), c->ev_iota.as<int32_t>(),
                                                       c->ev_slot_sorted.as<int32_t>(), (int)nkeys, lo_bit,
