@@ -205,9 +205,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
     constexpr int KN = sizeof(T) == 8 ? 4 * KS : NP;
     constexpr int kOut = (NB * NB + kConsWaves - 1) / kConsWaves;  // K output tiles per wave
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int t = a.batch_t0[a.batch] + blockIdx.x;
-    if (t >= a.batch_t0[a.batch + 1]) return;
-    const int r = a.td_r[t];
+    // the tile's pair count and relation from the gradient kernel (one load before
+    // the W0 staging), read beside the batch's tile range
+    const int cn = bf.cnrows[blockIdx.x];
+    if ((int)blockIdx.x >= a.batch_t0[a.batch + 1] - a.batch_t0[a.batch]) return;
+    const int r = cn >> 7;
     const int n = a.n, ld = a.ld;
     const int w = threadIdx.x >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
     T* Wl = (T*)smem;
@@ -218,7 +220,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
     const T lr = (T)a.lr;
     // this wave's pair rows (compacted by transr_grad_wave_kernel) and their a0 rows as
     // B fragments (not kept: the matrix partial re-reads them), loads issued before the barrier
-    const int nrows = bf.cnrows[blockIdx.x];
+    const int nrows = cn & 127;
     const int nblk = (nrows + 15) >> 4;
     const bool mine = w < nblk;  // this wave owns pair rows [16 w, 16 w + 16)
     const int32_t* cp = bf.cpairs + (int64_t)blockIdx.x * 2 * kCPairs;

@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void transr_grad_wave_kernel(RParArgs a, RParB
         } else if (slot >= 0) {
             bf.pflag[slot] = 0;
         }
-        if (l == 0) bf.cnrows[blockIdx.x] = __builtin_popcountll(m);
+        if (l == 0) bf.cnrows[blockIdx.x] = __builtin_popcountll(m) | (r << 7);  // rows | relation (cons kernel)
     }
 }
 
