@@ -209,7 +209,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
     // the W0 staging), read beside the batch's tile range
     const int cn = bf.cnrows[blockIdx.x];
     if ((int)blockIdx.x >= a.batch_t0[a.batch + 1] - a.batch_t0[a.batch]) return;
-    const int r = cn >> 7;
+    const int r = cn >> 8;
+    // the relation's only tile: its matrix partial goes straight into W'_r (the row
+    // pass would add this one partial to the same values), no partial round trip
+    const bool single = (cn >> 7) & 1;
     const int n = a.n, ld = a.ld;
     const int w = threadIdx.x >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
     T* Wl = (T*)smem;
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) bf.cons_tile[blockIdx.x] = misc[1];
+    if (threadIdx.x == 0) bf.cons_tile[blockIdx.x] = misc[1] && !single;
     if (!misc[1]) {  // no violator in the tile
         if (bf.stats && threadIdx.x == 0) {
             atomicAdd(&g_cons_stats[3], ck1 - ck0);
@@ -429,6 +432,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
     typename M::acc_t dw[kOut];
 #pragma unroll
     for (int q = 0; q < kOut; ++q) dw[q] = typename M::acc_t{T(0), T(0), T(0), T(0)};
+    // the relation's only tile: this lane's W'_r elements from the W0 image (= W'_r:
+    // nothing else writes the relation), read before the image is reused below
+    T wold[kOut][4];
+#pragma unroll
+    for (int q = 0; q < kOut; ++q) {
+        const int tile = w + kConsWaves * q;
+        const int jb = tile / NB, ib = tile % NB;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            wold[q][k] = (single && tile < NB * NB) ? Wl[(jb * 16 + M::row(l, k)) * L + ib * 16 + l16] : T(0);
+    }
     T* const CX = Wl;
     for (int c0 = 0; c0 < nblk; c0 += NB) {
         __syncthreads();  // the W0 / K reads (c0 = 0) or the previous chunks' reads are done
@@ -467,7 +481,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
             }
         }
     }
-    T* const wp = bf.wpart + (int64_t)blockIdx.x * n * ld;
+    T* const wp = single ? bf.W + (int64_t)r * n * ld : bf.wpart + (int64_t)blockIdx.x * n * ld;
 #pragma unroll
     for (int q = 0; q < kOut; ++q) {
         const int tile = w + kConsWaves * q;
@@ -477,7 +491,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void t
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int j = jb * 16 + M::row(l, k);
-            if (j < n && i < n) wp[(int64_t)j * ld + i] = -lr * dw[q][k];
+            if (j < n && i < n) wp[(int64_t)j * ld + i] = single ? wold[q][k] + -lr * dw[q][k] : -lr * dw[q][k];
         }
     }
     if (bf.stats && l == 0 && vm16) {

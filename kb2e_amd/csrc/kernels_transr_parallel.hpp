@@ -71,7 +71,7 @@ struct RParArgs {
     // tiles' relation, sample count, samples and rows without the index chain
     const int32_t* batch_t0;  // [nb + 1] first tile of each batch
     const int32_t* td_r;      // [tiles]
-    const int32_t* td_cnt;    // [tiles]
+    const int32_t* td_cnt;    // [tiles] samples | 256 when the tile is its relation's only one
     const int32_t* td_kk;     // [tiles][8] batch-local sample of tile sample q
     const int32_t* td_ent;    // [tiles][8][4] entity of row (q, h / t / h' / t'), -1 past cnt
 };
@@ -1070,7 +1070,8 @@ static __attribute__((unused)) __global__ __launch_bounds__(256) void rtile_desc
         const int f = tl.q * a.St, cnt = min(a.St, (p1 - p0) / 2 - f);
         if (q == 0) {
             a.td_r[t] = a.seg_row[tl.seg] - a.ne;
-            a.td_cnt[t] = cnt;
+            const bool single = a.tile_first[tl.seg + 1] - a.tile_first[tl.seg] == 1;
+            a.td_cnt[t] = cnt | (single ? 256 : 0);
         }
         int kk = 0, e4[4] = {-1, -1, -1, -1};
         if (q < cnt) {

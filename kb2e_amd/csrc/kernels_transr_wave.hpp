@@ -53,7 +53,7 @@ __global__ __launch_bounds__(128) void transr_proj_wave_kernel(RParArgs a, RParB
     // the tile from the per-epoch descriptors: two dependent loads to the rows
     const int t = a.batch_t0[a.batch] + blockIdx.x;
     if (t >= a.batch_t0[a.batch + 1]) return;
-    const int r = a.td_r[t], cnt = a.td_cnt[t];
+    const int r = a.td_r[t], cnt = a.td_cnt[t] & 255;
     const int n = a.n, ld = a.ld;
     const int w = threadIdx.x >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
     T* Wl = (T*)smem;
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void transr_grad_wave_kernel(RParArgs a, RParB
     constexpr int kSteps = 4;  // 2 St <= 16 updates (St <= 8 on the matrix-core path)
     const int t = a.batch_t0[a.batch] + blockIdx.x;
     if (t >= a.batch_t0[a.batch + 1]) return;
-    const int r = a.td_r[t], cnt = a.td_cnt[t];
+    const int r = a.td_r[t], cnt = a.td_cnt[t] & 255, single = (a.td_cnt[t] >> 8) & 1;
     const int n = a.n, ld = a.ld;
     const int w = threadIdx.x >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
     const int nu = 2 * cnt;
@@ -263,7 +263,8 @@ __global__ __launch_bounds__(256) void transr_grad_wave_kernel(RParArgs a, RParB
         } else if (slot >= 0) {
             bf.pflag[slot] = 0;
         }
-        if (l == 0) bf.cnrows[blockIdx.x] = __builtin_popcountll(m) | (r << 7);  // rows | relation (cons kernel)
+        // rows | the relation's only tile | relation, for the transRNorm kernel
+        if (l == 0) bf.cnrows[blockIdx.x] = __builtin_popcountll(m) | (single << 7) | (r << 8);
     }
 }
 
