@@ -104,7 +104,7 @@ struct kb2e_ctx {
     // device sampler (KB2E_SAMPLER_GLIBC): raw words of the glibc stream are
     // made on the host, the rejection chain is resolved on the device.
     hipStream_t side_stream = nullptr;
-    DevBuf words, levels, jfin, sidefin, filter_slots, pr_dev, consumed_dev;
+    DevBuf words, levels, jfin, sidefin, filter_slots, filter_bloom, pr_dev, consumed_dev;
     DevBuf trip;  // int4 per training triple: head, tail, relation, Bernoulli threshold (sample_len)
     DevBuf glibc_pow;  // M^(2^k) of the kGlibcBlock-word jump (glibc_starts_pow_kernel)
     DevBuf chain_table, chain_super, chain_sc, chain_ch, chain_overflow;  // the chain by chunks
@@ -568,6 +568,8 @@ void launch_prefetch(kb2e_ctx* c) {
     a.ne = c->cfg.num_entities;
     a.slots = c->filter_slots.as<uint64_t>();
     a.mask = c->ts.filter.mask;
+    a.bloom = c->filter_bloom.as<uint64_t>();
+    a.bloom_mask = c->ts.filter.bloom_mask;
     a.nr64 = (uint64_t)c->cfg.num_relations;
     a.ne64 = (uint64_t)c->cfg.num_entities;
     a.next = c->levels.as<int32_t>();
@@ -690,7 +692,9 @@ void start_epoch_stream(kb2e_ctx* c) {
         if (used >= 0) {
             c->rng.set_window(c->pin_win);  // the generator after the epoch's `used` words
             c->rng_version++;
-            c->words_per_sample = std::max(c->words_per_sample, 1.02 * (double)used / (double)c->S);
+            // the next epoch speculates on 3% (+ 4096) more words than this one used: every
+            // word position costs sample_len a triple gather and a filter probe
+            c->words_per_sample = 1.03 * (double)used / (double)c->S;
             break;
         }
         // the speculative word buffer ran out (long rejection runs): retry larger
@@ -1281,6 +1285,9 @@ kb2e_status kb2e_upload_triples(kb2e_ctx* c, const int32_t* h, const int32_t* t,
         HIPCHK(hipMemcpy(c->rels.p, r, count * 4, hipMemcpyHostToDevice));
         c->filter_slots.alloc(c->ts.filter.slots.size() * 8);
         HIPCHK(hipMemcpy(c->filter_slots.p, c->ts.filter.slots.data(), c->ts.filter.slots.size() * 8,
+                         hipMemcpyHostToDevice));
+        c->filter_bloom.alloc(c->ts.filter.bloom.size() * 8);
+        HIPCHK(hipMemcpy(c->filter_bloom.p, c->ts.filter.bloom.data(), c->ts.filter.bloom.size() * 8,
                          hipMemcpyHostToDevice));
         std::vector<double> pr(c->ts.pr);
         if (c->cfg.method == 0) std::fill(pr.begin(), pr.end(), 500.0);  // common/trainer.cpp:84-86

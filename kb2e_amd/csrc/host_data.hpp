@@ -30,8 +30,15 @@ struct FilterSet {
     std::vector<uint64_t> slots;
     uint64_t mask = 0;
     uint64_t ne = 1, nr = 1;
+    // Blocked Bloom prefilter for the device sampler (>= 12 bits a key, two bits
+    // in one 64-bit word): a corrupted triple almost never is a training triple,
+    // so sample_len answers most probes from this L2-sized array instead of a
+    // random line of `slots`.  No false negatives: results are unchanged.
+    std::vector<uint64_t> bloom;
+    uint64_t bloom_mask = 0;
 
     static constexpr uint64_t kEmpty = ~0ull;
+    static constexpr uint64_t kBloomSalt = 0x9e3779b97f4a7c15ull;
 
     uint64_t key(int64_t h, int64_t r, int64_t t) const {
         return ((uint64_t)h * nr + (uint64_t)r) * ne + (uint64_t)t;
@@ -46,6 +53,14 @@ struct FilterSet {
         slots.assign(cap, kEmpty);
         mask = cap - 1;
         for (size_t k = 0; k < H.size(); ++k) insert(key(H[k], R[k], T[k]));
+        uint64_t nw = 64;
+        while (nw * 64 < 12 * (uint64_t)H.size()) nw <<= 1;
+        bloom.assign(nw, 0);
+        bloom_mask = nw - 1;
+        for (size_t k = 0; k < H.size(); ++k) {
+            const uint64_t b = mix64(key(H[k], R[k], T[k]) ^ kBloomSalt);
+            bloom[b & bloom_mask] |= (1ull << ((b >> 52) & 63)) | (1ull << (b >> 58));
+        }
     }
 
     void insert(uint64_t k) {

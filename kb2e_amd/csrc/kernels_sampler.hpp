@@ -39,6 +39,8 @@ struct SamplerArgs {
     int32_t ntrain, ne;
     const uint64_t* slots;  // filter hash table
     uint64_t mask;
+    const uint64_t* bloom;  // FilterSet::bloom (host_data.hpp): two bits a key in one word
+    uint64_t bloom_mask;
     uint64_t nr64, ne64;
     int32_t* next;          // [nraw + 1]
     int32_t* jfin;          // [nraw]
@@ -56,6 +58,9 @@ __device__ __forceinline__ uint64_t dev_mix64(uint64_t x) {
 
 __device__ __forceinline__ bool filter_has(const SamplerArgs& a, int64_t h, int64_t r, int64_t t) {
     const uint64_t k = ((uint64_t)h * a.nr64 + (uint64_t)r) * a.ne64 + (uint64_t)t;
+    const uint64_t b = dev_mix64(k ^ 0x9e3779b97f4a7c15ull);  // FilterSet::kBloomSalt
+    const uint64_t bits = (1ull << ((b >> 52) & 63)) | (1ull << (b >> 58));
+    if ((a.bloom[b & a.bloom_mask] & bits) != bits) return false;
     uint64_t p = dev_mix64(k) & a.mask;
     while (true) {
         const uint64_t s = a.slots[p];
