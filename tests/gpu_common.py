@@ -28,13 +28,13 @@ def tiny():
     return data.load(os.path.join(GOLDEN, "tiny"))
 
 
-def golden_engine(name, precision=64, sampler=SAMPLER_GLIBC):
+def golden_engine(name, precision=64, sampler=SAMPLER_GLIBC, schedule="ordered"):
     run = MANIFEST["runs"][name]
     f = run["flags"]
     ds = tiny()
     eng = Engine(run["model"], f["size"], ds.num_entities, ds.num_relations, rate=f["rate"], margin=f["margin"],
                  method=f["method"], distance=f["distance"], batches=f["batches"], seed=f["seed"],
-                 precision=precision, sampler=sampler, transr_compat=not run["transr_fixed"])
+                 precision=precision, sampler=sampler, transr_compat=not run["transr_fixed"], schedule=schedule)
     eng.upload_triples(ds.train)
     init = eng.init_params()
     if run["model"] == "R":
