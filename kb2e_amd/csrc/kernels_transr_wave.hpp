@@ -211,10 +211,10 @@ __global__ __launch_bounds__(256) void transr_grad_wave_kernel(RParArgs a, RParB
             if (M::row(l, 0) == 0 && i < n) bf.rpart[(int64_t)blockIdx.x * ld + i] = dr[0];
         }
     }
-    if (threadIdx.x == 0) {  // the tile's active updates
-        int nact = 0;
-        for (int u = 0; u < nu; ++u) nact += a.act[a.td_kk[t * 8 + (u >> 1)]] != 0;
-        a.tile_act[t] = nact;
+    if (w == 0) {  // the tile's active updates: lane u holds update u (nu <= 16), one ballot
+        const bool au = l < nu && a.act[a.td_kk[t * 8 + (l >> 1)]] != 0;
+        const uint64_t m = __ballot(au);
+        if (l == 0) a.tile_act[t] = __builtin_popcountll(m);
     }
     if (w == kConsWaves - 1) {
         // the tile's transRNorm pairs for transr_cons_wave_kernel: (h', r), (t', r) of the
