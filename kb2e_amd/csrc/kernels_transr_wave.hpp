@@ -42,10 +42,18 @@ __device__ __forceinline__ double quad_bcast(double x) {
 
 constexpr int kProjWaves = 2;  // 4 St <= 32 rows: two 16-row blocks
 
+// W0 rows transr_proj_wave_kernel stages: FP64 reads rows k = kmap(s, kq) < 4 KS
+// only (rows >= n are zero, so the y product masks the rest instead of reading
+// them: 27.5 KB instead of 34 KB at n = 50, five workgroups a CU instead of four)
+template <typename T>
+__host__ __device__ constexpr int proj_wave_rows(int KS) {
+    return sizeof(T) == 8 ? 4 * KS : 16 * ((KS + 3) / 4);
+}
+
 template <typename T, int KS>
 __global__ __launch_bounds__(128) void transr_proj_wave_kernel(RParArgs a, RParBufs<T> bf) {
     using M = Mfma16<T>;
-    constexpr int NB = (KS + 3) / 4, NP = 16 * NB, L = NP + 2, NS = NP / 4;
+    constexpr int NB = (KS + 3) / 4, NP = 16 * NB, L = NP + 2, NS = NP / 4, R = proj_wave_rows<T>(KS);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // fixed energy: this kernel fills the pair-dedupe table (every thread of the grid
     // clears its share of the next batch's first)
@@ -65,7 +73,7 @@ __global__ __launch_bounds__(128) void transr_proj_wave_kernel(RParArgs a, RParB
     const int e = ed < 0 ? 0 : ed;
     {  // W0 as element pairs, every load in flight before the LDS stores
         using T2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
-        constexpr int kPairs = NP * L / 2, kThreads = kProjWaves * kWave;
+        constexpr int kPairs = R * L / 2, kThreads = kProjWaves * kWave;
         constexpr int kPer = (kPairs + kThreads - 1) / kThreads;
         const T2* Wg = (const T2*)(bf.W + (int64_t)r * n * ld);
         const int hp = ld / 2;
@@ -151,7 +159,10 @@ __global__ __launch_bounds__(128) void transr_proj_wave_kernel(RParArgs a, RParB
     for (int jb = 0; jb < NB; ++jb) {
         typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
 #pragma unroll
-        for (int s = 0; s < KS; ++s) acc = M::mma(Wl[(jb * 16 + l16) * L + kmap<T>(s, kq)], xf[s], acc);
+        for (int s = 0; s < KS; ++s) {
+            const int jr = jb * 16 + l16;  // rows >= R (all >= n) are zero
+            acc = M::mma(jr < R ? Wl[jr * L + kmap<T>(s, kq)] : T(0), xf[s], acc);
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int j = jb * 16 + M::row(l, k);

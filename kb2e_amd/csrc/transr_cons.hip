@@ -74,7 +74,7 @@ void proj_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, hipStr
     RParArgs aa = a;
     RParBufs<T> bb = bf;
     void* args[] = {&aa, &bb};
-    const size_t lds = sizeof(T) * (size_t)rm_np(a.n) * rm_ld(a.n);
+    const size_t lds = sizeof(T) * (size_t)proj_wave_rows<T>(cons_live_steps<T>(a.n)) * rm_ld(a.n);
     HIPCHK(hipLaunchKernel(kernel_fn<T>(kProj, a.n), dim3(grid), dim3(kProjWaves * kWave), args, lds, stream));
 }
 
