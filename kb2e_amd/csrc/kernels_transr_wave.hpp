@@ -19,8 +19,8 @@
 // in one DPP quad of every lane group, so d_p = p_t - p_h - r and x (the L1
 // sign / L2 2 d_p), the energies and the raw d = h - t come from quad_perm
 // moves, y = W0 x is the MFMA product Y^T = W0 X^T with the x fragments as
-// the B operand, and only W0 is staged in LDS (34 KB at n = 50: four
-// workgroups of two waves per CU).
+// the B operand, and only W0 is staged in LDS (its live rows, 27.5 KB at
+// n = 50: five workgroups of two waves per CU).
 #pragma once
 
 #include "kernels_transr_cons.hpp"
