@@ -48,7 +48,7 @@ kb2e_amd/build/transr_cons.o: kb2e_amd/csrc/transr_cons.hip kb2e_amd/csrc/transr
 	$(HIPCC) $(HIPFLAGS) -c -o $@ kb2e_amd/csrc/transr_cons.hip
 
 kb2e_amd/libkb2e.so: kb2e_amd/build/engine.o kb2e_amd/build/eval.o kb2e_amd/build/textio.o kb2e_amd/build/transr_cons.o
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 # diagnostic build: per-phase cycle counters in the relation-owner kernels
 prof: kb2e_amd/libkb2e_prof.so
@@ -59,7 +59,7 @@ kb2e_amd/build/engine_prof.o: $(CSRC)
 
 kb2e_amd/libkb2e_prof.so: kb2e_amd/build/engine_prof.o kb2e_amd/build/eval.o kb2e_amd/build/textio.o \
 		kb2e_amd/build/transr_cons.o
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -C oracle all

@@ -30,7 +30,8 @@ N>1 (torchrun): each rank owns the triples whose head hashes to it
  and runs batches of the single-GPU size over its shard
 (100 / N batches per epoch), so per-GPU work per step is fixed (weak scaling);
 at every epoch boundary the ranks sum their table deltas over RCCL and
-re-apply the norm constraints (kb2e_amd.distributed).
+re-apply the norm constraints inside the engine (kb2e_merge_epoch, its own
+RCCL communicator; kb2e_amd.distributed.NativeMerger).
 """
 import argparse
 import json
@@ -111,23 +112,54 @@ def algorithmic_bytes_per_sample(model, n, s, active_frac):
     return full, 20 + (n * n + 5 * n) * s, active_frac * (2 * n * n + 10 * n) * s
 
 
-def _ref_epoch_seconds(cmd, e1, e2, limit_s):
-    """Seconds per epoch of the reference binary on one core:
-    (wall(e2 epochs) - wall(e1 epochs)) / (e2 - e1), so data loading,
-    initialisation and writing the output files cancel out."""
+def _ref_epoch_seconds(cmd, epochs, limit_s):
+    """Seconds per epoch of the reference binary on one core, from the
+    timestamps of its `Epoch: %d, Loss: %f` lines (common/trainer.cpp:105),
+    read through a pseudo-terminal so its stdout is line-buffered: the mean
+    over epochs 1..epochs-1 (epoch 0 and the data loading / init before it are
+    excluded)."""
+    import pty
+    import select
+
     cpu = min(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
 
     def pin():
         if cpu is not None:
             os.sched_setaffinity(0, {cpu})
 
-    wall = []
-    for e in (e1, e2):
-        t0 = time.perf_counter()
-        subprocess.run(cmd + ["--epochs", str(e)], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                       timeout=limit_s, preexec_fn=pin, check=True)
-        wall.append(time.perf_counter() - t0)
-    return (wall[1] - wall[0]) / (e2 - e1)
+    master, slave = pty.openpty()
+    p = subprocess.Popen(cmd + ["--epochs", str(epochs)], stdout=slave, stderr=subprocess.DEVNULL,
+                         stdin=subprocess.DEVNULL, preexec_fn=pin, close_fds=True)
+    os.close(slave)
+    stamps, buf, t_end = {}, b"", time.perf_counter() + limit_s
+    try:
+        while time.perf_counter() < t_end:
+            r, _, _ = select.select([master], [], [], 1.0)
+            if not r:
+                if p.poll() is not None:
+                    break
+                continue
+            try:
+                chunk = os.read(master, 4096)
+            except OSError:  # EIO: the child closed the terminal
+                break
+            if not chunk:
+                break
+            now = time.perf_counter()
+            buf += chunk
+            while b"\n" in buf:
+                line, buf = buf.split(b"\n", 1)
+                if line.startswith(b"Epoch: "):
+                    stamps[int(line.split(b",")[0][7:])] = now
+    finally:
+        if p.poll() is None:
+            p.kill()
+        p.wait()
+        os.close(master)
+    last = max(stamps) if stamps else -1
+    if last < 1 or 0 not in stamps:
+        raise RuntimeError(f"reference printed epochs {sorted(stamps)} within {limit_s} s")
+    return (stamps[last] - stamps[0]) / last, last
 
 
 def cpu_baseline(cfg_name, ds, seed_dir=None, budget_s=25.0):
@@ -138,8 +170,8 @@ def cpu_baseline(cfg_name, ds, seed_dir=None, budget_s=25.0):
     binary = os.path.join(ROOT, "oracle", "_ref", {"E": "trainTransE", "H": "trainTransH", "R": "trainTransR"}[model])
     S = (len(ds.train) // 100) * 100
     if os.path.exists(binary):
-        # (e1, e2) epochs: wall(e2) - wall(e1) keeps ~5-15 s of training
-        e1, e2 = {"E": (0, 8), "H": (0, 4), "R": (0, 1)}[model]
+        # epochs 1..E-1 timed (>= 3): ~10-40 s of training
+        epochs = {"E": 9, "H": 6, "R": 4}[model]
         with tempfile.TemporaryDirectory() as d:
             data.write(ds, d)
             cmd = [binary, "--datadir", d, "--outdir", d, "--size", str(dim), "--method", str(method),
@@ -149,11 +181,11 @@ def cpu_baseline(cfg_name, ds, seed_dir=None, budget_s=25.0):
                 # the same TransE seed files the GPU run read (transr/trainer.cpp:88-113)
                 cmd += ["--seeddatadir", seed_dir, "--seedmethod", "0"]
                 seed_note = f", seeded from the GPU run's TransE-init files ({SEED_EPOCHS} TransE epochs)"
-            per_epoch = _ref_epoch_seconds(cmd, e1, e2, budget_s * 4)
+            per_epoch, timed = _ref_epoch_seconds(cmd, epochs, budget_s * 8)
         return {"value": S / per_epoch, "unit": "triples/s", "cores": 1, "kind": "reference", **host_cpu(),
                 "sample": f"{os.path.basename(binary)} (compiled from the reference sources) on the same synthetic "
-                          f"{shape}-shaped data{seed_note}, 1 thread pinned to one core; per-epoch time = (wall of "
-                          f"{e2} epochs - wall of {e1}) / {e2 - e1}, {S} samples per epoch"}
+                          f"{shape}-shaped data{seed_note}, 1 thread pinned to one core; mean time of epochs 1..{timed} "
+                          f"from the timestamps of its Epoch lines (epoch 0 and init excluded), {S} samples per epoch"}
     from oracle import orc  # CPU restatement (port) fallback
     m = orc.Model(model, dim, ds.num_entities, ds.num_relations, rate=rate, method=method, distance=distance,
                   batches=100)
@@ -207,8 +239,8 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
     B = len(train) // batches
     merger = None
     if world > 1:
-        from kb2e_amd.distributed import EpochMerger
-        merger = EpochMerger(eng, dist)
+        from kb2e_amd.distributed import make_merger
+        merger = make_merger(eng, dist)  # RCCL inside the engine (kb2e_merge_epoch); gloo: torch-side
 
     def run(k_steps):
         done = 0

@@ -223,15 +223,51 @@ kb2e_status kb2e_profile_query(kb2e_ctx* ctx, const char* name, double* total_ms
 /* Device memory footprint in bytes (tables + work buffers). */
 int64_t kb2e_device_bytes(const kb2e_ctx* ctx);
 
-/* Multi-GPU (one context per rank): raw device pointers of the parameter
- * tables and their element counts, so a communicator (RCCL via
- * torch.distributed) can reduce deltas in place; kb2e_merge_epoch re-applies
- * the reference's norm constraints after a merge. */
+/* Multi-GPU epoch merge (the reference is single-process, so
+ * this replaces no reference call: it is the exchange step that lets N
+ * contexts, each training a head-hash shard of the triples with the
+ * single-GPU schedule, act as one trainer).  At an epoch boundary every rank
+ * holds T_r; the merge sets, on every rank,
+ *     T <- renorm(T0 + sum_r (T_r - T0))
+ * where T0 is the tables after the previous merge: the entity deltas are
+ * reduce-scattered to the owner of each block of rows over RCCL, the owner
+ * adds them and re-applies the model's norm constraint to the rows any rank
+ * changed (as kb2e_renormalize), and an all-gather returns the merged table;
+ * relation and weight deltas are all-reduced and every rank renormalises the
+ * changed rows.  All work runs on the contexts' own streams; the calls return
+ * when the merged tables are in place.  Two ways to build the communicator:
+ *  - one process per GPU (torchrun): rank 0 makes an id with
+ *    kb2e_comm_unique_id, the caller hands it to every rank (any side channel),
+ *    and each rank calls kb2e_comm_init_rank (collective) and then
+ *    kb2e_merge_epoch at every epoch boundary (collective);
+ *  - one process driving N devices (one host thread, SURVEY.md 8(b)
+ *    "Threading"): kb2e_comm_init_group over the N contexts, then
+ *    kb2e_merge_epoch_group.  Contexts that share a device (or
+ *    KB2E_MERGE_LOCAL=1) merge with plain device kernels instead of RCCL, which
+ *    refuses two ranks on one GPU.
+ * Initialisation broadcasts rank 0's tables to every rank, so the ranks may
+ * be created with different seeds (distinct sample streams).  The contexts must
+ * agree on model, dim, table sizes and precision; their tables must be loaded
+ * (kb2e_init_params / kb2e_upload_params / kb2e_transr_seed) first. */
+#define KB2E_COMM_ID_BYTES 128
+kb2e_status kb2e_comm_unique_id(uint8_t* id /* KB2E_COMM_ID_BYTES */);
+kb2e_status kb2e_comm_init_rank(kb2e_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* id);
+kb2e_status kb2e_comm_init_group(kb2e_ctx* const* ctxs, int32_t n);
+kb2e_status kb2e_merge_epoch(kb2e_ctx* ctx);
+kb2e_status kb2e_merge_epoch_group(kb2e_ctx* const* ctxs, int32_t n);
+/* This rank's place in the communicator and the entity rows it owns in the merge. */
+kb2e_status kb2e_comm_info(kb2e_ctx* ctx, int32_t* nranks, int32_t* rank, int64_t* first_entity,
+                           int64_t* entity_count);
+
+/* Raw device pointers of the parameter tables (row-major, leading dimension
+ * round_up(dim, 2), FP64 or FP32 by precision) and their element counts, for a
+ * caller-side communicator (kb2e_amd/distributed.py: torch.distributed gloo in
+ * the CPU tests). */
 kb2e_status kb2e_device_tables(kb2e_ctx* ctx, void** entity, void** relation, void** weights,
                                int64_t* n_entity, int64_t* n_relation, int64_t* n_weights);
-/* Re-apply the per-row norm constraints of the model after a merge, to the
- * rows flagged non-zero in the host masks (NULL = every row): TransE rows and
- * TransH entity/relation rows are shrunk to length <= 1 (common/utils.cpp:70-77),
+/* Re-apply the per-row norm constraints of the model, to the rows flagged
+ * non-zero in the host masks (NULL = every row): TransE rows and TransH
+ * entity/relation rows are shrunk to length <= 1 (common/utils.cpp:70-77),
  * TransH normals and TransR entity/relation/matrix rows scaled to unit length
  * (transh/trainer.cpp:52, transr/trainer.cpp:174-180).  Weight masks are per
  * relation. */
@@ -239,10 +275,8 @@ kb2e_status kb2e_renormalize(kb2e_ctx* ctx, const uint8_t* entity_rows, const ui
                              const uint8_t* weight_rows);
 /* The same constraint on `count` units of one table from `first` (table 0:
  * entities, 1: relations, 2: weights, in relations), with the row mask in
- * DEVICE memory (device_mask[k] for unit first + k; NULL = every row), so a
- * merge that computed the changed rows on the device never copies to the host
- * (kb2e_amd/distributed.py: each rank renormalises the entity block it owns
- * after a reduce-scatter). */
+ * DEVICE memory (device_mask[k] for unit first + k; NULL = every row).
+ * Returns when the rows are renormalised. */
 kb2e_status kb2e_renormalize_rows(kb2e_ctx* ctx, int32_t table, int64_t first, int64_t count,
                                   const uint8_t* device_mask);
 

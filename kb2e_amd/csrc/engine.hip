@@ -62,6 +62,8 @@ struct Timer {
 }  // namespace
 
 struct kb2e_ctx;
+struct MergeState;               // engine_merge.inc
+void merge_free(MergeState* m);  // engine_merge.inc
 namespace {
 void setup_relowner_buffers(kb2e_ctx* c);
 template <typename T>
@@ -189,8 +191,11 @@ struct kb2e_ctx {
     };
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
+    // multi-GPU epoch merge (engine_merge.inc): communicator, base tables, buffers
+    MergeState* mg = nullptr;
 
     ~kb2e_ctx() {
+        if (mg) merge_free(mg);
         if (pin_si) (void)hipHostFree(pin_si);
         if (pin_sj) (void)hipHostFree(pin_sj);
         if (pin_side) (void)hipHostFree(pin_side);
@@ -1597,6 +1602,9 @@ kb2e_status kb2e_train_batches(kb2e_ctx* c, int32_t nbatches) {
 kb2e_status kb2e_synchronize(kb2e_ctx* c) {
     return guarded(c, [&] {
         HIPCHK(hipStreamSynchronize(c->stream));
+        // the next epoch's sampling / index, queued on the side stream during
+        // this one, is part of the work the caller waits for
+        if (c->side_stream) HIPCHK(hipStreamSynchronize(c->side_stream));
         return KB2E_OK;
     });
 }
@@ -1800,10 +1808,12 @@ kb2e_status kb2e_renormalize_rows(kb2e_ctx* c, int32_t table, int64_t first, int
         if (first < 0 || count < 0 || first + count > units) return fail(c, KB2E_EINVAL, "rows out of range");
         HIPCHK(hipSetDevice(c->cfg.device));
         renorm_rows(c, table, first, count, device_mask);
-        if (table == 2) sync_wsnap(c);
-        else HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (table == 2) sync_wsnap(c);  // TransR: the committed matrices follow
         return KB2E_OK;
     });
 }
 
 }  // extern "C"
+
+#include "engine_merge.inc"

@@ -12,7 +12,9 @@
 // per-row deltas with one norm per batch, kb2e_engine.h kb2e_schedule).
 #include <sys/stat.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -50,6 +52,7 @@ struct EmbeddingArguments {  // common/args.h:9-25, defaults common/constants.h:
     int device = 0;
     int transrCompat = 1;
     int schedule = 0;
+    int gpus = 1;
 
     std::string to_string() const {  // common/args.cpp:33-50
         std::string r = "Options: [";
@@ -104,6 +107,7 @@ void printUsage(const char* invoked) {  // common/args.cpp:125-142
     printf("   --device [0] (GPU ordinal)\n");
     printf("   --transrcompat [1] (TransR: reproduce the accumulating energy)\n");
     printf("   --schedule [0] (GPU: 0 ordered = the reference's sequence, 1 parallel)\n");
+    printf("   --gpus [1] (GPU: devices --device .. --device+N-1, triples sharded by head, epoch merge over RCCL)\n");
 }
 
 EmbeddingArguments parseArgs(int argc, char** argv) {  // common/args.cpp:53-122
@@ -129,6 +133,7 @@ EmbeddingArguments parseArgs(int argc, char** argv) {  // common/args.cpp:53-122
     if ((i = argpos("device", true, argc, argv)) != -1) a.device = atoi(argv[i + 1]);
     if ((i = argpos("transrcompat", true, argc, argv)) != -1) a.transrCompat = atoi(argv[i + 1]);
     if ((i = argpos("schedule", true, argc, argv)) != -1) a.schedule = atoi(argv[i + 1]) ? 1 : 0;
+    if ((i = argpos("gpus", true, argc, argv)) != -1) a.gpus = std::max(1, atoi(argv[i + 1]));
     return a;
 }
 
@@ -210,7 +215,7 @@ class Trainer {  // the interface of common::Trainer (common/trainer.h:14-78)
    public:
     Trainer(EmbeddingArguments args, kb2e_model model) : args_(args), model_(model) {}
     virtual ~Trainer() {
-        if (ctx_) kb2e_destroy(ctx_);
+        for (kb2e_ctx* c : ranks_) kb2e_destroy(c);
     }
 
     void add(int head, int tail, int relation) {
@@ -233,6 +238,8 @@ class Trainer {  // the interface of common::Trainer (common/trainer.h:14-78)
 
     void train() {  // common/trainer.cpp:60-63
         prepTrain();
+        if (ranks_.size() > 1)  // rank 0's tables everywhere, the merge's communicator
+            check(ctx_, kb2e_comm_init_group(ranks_.data(), (int32_t)ranks_.size()), "comm_init_group");
         bfgs();
     }
 
@@ -246,13 +253,63 @@ class Trainer {  // the interface of common::Trainer (common/trainer.h:14-78)
    protected:
     EmbeddingArguments args_;
     kb2e_model model_;
-    kb2e_ctx* ctx_ = nullptr;
+    kb2e_ctx* ctx_ = nullptr;          // rank 0 (the tables write() prints)
+    std::vector<kb2e_ctx*> ranks_;     // one context per GPU (--gpus)
     int numRelations_ = 0, numEntities_ = 0;
     std::vector<int> heads_, tails_, relations_;
 
     // common/trainer.cpp:34-58: the initial tables, drawn from the same
-    // glibc stream (seeded with --seed) inside the engine.
+    // glibc stream (seeded with --seed) inside the engine.  --gpus N: one
+    // context per device, each training the triples whose head hashes to it
+    //  in batches of the single-GPU size (numBatches / N
+    // batches an epoch), rank k seeded with seed + k (distinct sample streams;
+    // the merge starts every rank from rank 0's tables).
     virtual void prepTrain() {
+        const int N = args_.gpus;
+        for (int k = 0; k < N; ++k) {
+            std::vector<int> h, t, r;
+            for (size_t i = 0; i < heads_.size(); ++i)
+                if (N == 1 || head_owner(heads_[i], N) == k) {
+                    h.push_back(heads_[i]);
+                    t.push_back(tails_[i]);
+                    r.push_back(relations_[i]);
+                }
+            ranks_.push_back(make_rank(k, h, t, r));
+        }
+        ctx_ = ranks_[0];
+    }
+
+    // common/trainer.cpp:69-107, on the GPU.
+    virtual void bfgs() {
+        const int32_t nb = (int32_t)std::max(1, args_.numBatches / args_.gpus);
+        for (int epoch = 0; epoch < args_.maxEpochs; epoch++) {
+            double loss = 0;
+            int64_t active = 0;
+            if (ranks_.size() == 1) {
+                check(ctx_, kb2e_train_epoch(ctx_, &loss, &active), "train_epoch");
+            } else {
+                for (kb2e_ctx* c : ranks_) check(c, kb2e_train_batches(c, nb), "train_batches");  // queued
+                for (kb2e_ctx* c : ranks_) {
+                    double l = 0;
+                    int64_t a = 0;
+                    check(c, kb2e_take_stats(c, &l, &a), "take_stats");
+                    loss += l;
+                    active += a;
+                }
+                check(ctx_, kb2e_merge_epoch_group(ranks_.data(), (int32_t)ranks_.size()), "merge_epoch");
+            }
+            printf("Epoch: %d, Loss: %f\n", epoch, loss);
+            fflush(stdout);
+        }
+    }
+
+    // the shard owner of a head entity (kb2e_amd/distributed.py shard_heads)
+    static int head_owner(int head, int world) {
+        const uint64_t h = (uint64_t)(uint32_t)head * 0x9E3779B97F4A7C15ull;
+        return (int)((h >> 40) % (uint64_t)world);
+    }
+
+    kb2e_ctx* make_rank(int k, const std::vector<int>& h, const std::vector<int>& t, const std::vector<int>& r) {
         kb2e_config cfg;
         kb2e_default_config(&cfg);
         cfg.model = model_;
@@ -263,30 +320,39 @@ class Trainer {  // the interface of common::Trainer (common/trainer.h:14-78)
         cfg.margin = args_.margin;
         cfg.method = args_.method;
         cfg.distance = args_.distanceType;
-        cfg.num_batches = args_.numBatches;
-        cfg.seed = args_.seed;
+        cfg.num_batches = std::max(1, args_.numBatches / args_.gpus);
+        cfg.seed = args_.seed + (unsigned)k;
         cfg.precision = args_.precision;
-        cfg.device = args_.device;
+        // KB2E_CLI_ONE_DEVICE=1: every rank on --device (the one-GPU test box; the
+        // merge then runs on the engine's local backend instead of RCCL)
+        const char* one = getenv("KB2E_CLI_ONE_DEVICE");
+        cfg.device = (one && one[0] == '1') ? args_.device : args_.device + k;
         cfg.transr_compat = args_.transrCompat;
         cfg.schedule = args_.schedule ? KB2E_SCHEDULE_PARALLEL : KB2E_SCHEDULE_ORDERED;
-        check(nullptr, kb2e_create(&cfg, &ctx_), "create");
-        check(ctx_, kb2e_upload_triples(ctx_, heads_.data(), tails_.data(), relations_.data(), (int64_t)heads_.size()),
-              "upload_triples");
+        if (h.empty()) {
+            printf("kb2e: GPU %d has no training triples (--gpus %d)\n", k, args_.gpus);
+            exit(1);
+        }
+        kb2e_ctx* c = nullptr;
+        check(nullptr, kb2e_create(&cfg, &c), "create");
+        check(c, kb2e_upload_triples(c, h.data(), t.data(), r.data(), (int64_t)h.size()), "upload_triples");
         // the reference's randn draws and row norms, made on the device from the
         // same stream (kb2e_init_params is the host form of the same thing)
         int64_t ties = 0;
-        check(ctx_, kb2e_init_params_device(ctx_, nullptr, nullptr, nullptr, &ties), "init_params");
-    }
-
-    // common/trainer.cpp:69-107, on the GPU.
-    virtual void bfgs() {
-        for (int epoch = 0; epoch < args_.maxEpochs; epoch++) {
-            double loss = 0;
-            int64_t active = 0;
-            check(ctx_, kb2e_train_epoch(ctx_, &loss, &active), "train_epoch");
-            printf("Epoch: %d, Loss: %f\n", epoch, loss);
-            fflush(stdout);
+        check(c, kb2e_init_params_device(c, nullptr, nullptr, nullptr, &ties), "init_params");
+        if (ties > 0) {
+            // an accept/reject decision sat within a few ulps of the density, where
+            // the device exp could round unlike glibc's: redo the init on the host
+            // (exact) from a fresh context, so the stream position is the reference's
+            fprintf(stderr, "kb2e: %lld near-tie randn decisions on the device; initialising on the host\n",
+                    (long long)ties);
+            kb2e_destroy(c);
+            c = nullptr;
+            check(nullptr, kb2e_create(&cfg, &c), "create");
+            check(c, kb2e_upload_triples(c, h.data(), t.data(), r.data(), (int64_t)h.size()), "upload_triples");
+            check(c, kb2e_init_params(c, nullptr, nullptr, nullptr), "init_params");
         }
+        return c;
     }
 };
 
@@ -311,6 +377,7 @@ class TransRTrainer : public Trainer {
     void prepTrain() override {  // transr/trainer.cpp:70-114
         Trainer::prepTrain();
         // seed files parsed on the device; entities unit-normed, relations verbatim
+        // (rank 0's tables are broadcast to the other ranks by the merge's init)
         std::string path = args_.seedDataDir + "/entity2vec." + method_name(args_.seedMethod);
         readSeed(ctx_, 0, path, KB2E_READ_UNIT);
         path = args_.seedDataDir + "/relation2vec." + method_name(args_.seedMethod);

@@ -16,9 +16,16 @@ table deltas and re-apply the reference's norm constraints:
   all-gather hands every rank the merged table -- the all-reduce's bytes, but
   each rank renormalises only 1/N of the rows.
 
-The changed-row masks are computed and consumed on the device
-(kb2e_renormalize_rows takes a device mask): no host copy, no host sync beyond
-the collectives themselves.  Rows touched by one rank get exactly that rank's
+Two implementations of the same merge:
+
+* `NativeMerger` (the product path, RCCL): the merge runs inside the engine
+  (kb2e_comm_init_rank / kb2e_merge_epoch, engine_merge.inc) on the engine's
+  own stream over the engine's own RCCL communicator; torch.distributed only
+  hands rank 0's communicator id to the other ranks.
+* `EpochMerger` / `TableMerger` (gloo: the CPU tests and the one-GPU
+  rehearsal, where RCCL refuses two ranks on one device): the same phases
+  over torch tensors that alias the engine's tables, with the changed-row
+  masks on the device (kb2e_renormalize_rows takes a device mask).  Rows touched by one rank get exactly that rank's
 update; shared rows (popular relations) get every rank's contribution, like a
 sequential pass over the shards.  This is a documented relaxation of the
 single-GPU semantics (local SGD per epoch); single-GPU runs are exact.
@@ -70,7 +77,8 @@ class _EngineRows:
     def renormalize(self, table, first, count, mask):
         import torch
 
-        torch.cuda.synchronize()  # torch's stream wrote the rows; the engine's stream renormalises them
+        if mask is not None and mask.is_cuda:
+            torch.cuda.synchronize()  # torch's stream wrote the rows; the engine's stream renormalises them
         self.eng.renormalize_rows(table, first, count, mask.data_ptr() if mask is not None else None)
 
 
@@ -123,6 +131,7 @@ class TableMerger:
         for t in tables:  # every rank starts from rank 0's tables
             dist.broadcast(t, 0)
         self.base = [t.clone() for t in tables]
+        self._torch_sync(tables[0])  # the engine's stream must not run before torch's copies land
         ne, L = units[0], unit_len[0]
         self.block = (ne + self.world - 1) // self.world  # entity rows per owner
         self.lo = min(ne, self.rank * self.block)
@@ -160,6 +169,14 @@ class TableMerger:
         self.rows.synchronize()
         for t, b in zip(self.tables, self.base):
             b.copy_(t)
+        self._torch_sync(self.tables[0])  # the next batches (engine stream) write the tables
+
+    @staticmethod
+    def _torch_sync(t):
+        if t.is_cuda:
+            import torch
+
+            torch.cuda.synchronize()
 
 
 class EpochMerger(TableMerger):
@@ -171,6 +188,37 @@ class EpochMerger(TableMerger):
         units = [eng.ne, eng.nr] + ([eng.nr] if len(tables) > 2 else [])
         unit_len = [ld, ld] + ([tables[2].numel() // eng.nr] if len(tables) > 2 else [])
         super().__init__(tables, units, unit_len, _EngineRows(eng), dist)
+
+
+class NativeMerger:
+    """The epoch merge inside the engine over its own RCCL communicator
+    (kb2e_comm_init_rank + kb2e_merge_epoch): rank 0 makes the RCCL id, the
+    torch process group broadcasts it, every rank joins (rank 0's tables are
+    broadcast by the engine)."""
+
+    def __init__(self, eng, dist):
+        import torch
+
+        from .engine import COMM_ID_BYTES, Engine
+
+        rank, world = dist.get_rank(), dist.get_world_size()
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        buf = torch.zeros(COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            buf.copy_(torch.tensor(list(Engine.comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(buf, 0)
+        eng.comm_init_rank(world, rank, bytes(buf.cpu().tolist()))
+        self.eng = eng
+
+    def merge(self):
+        self.eng.merge_epoch()
+
+
+def make_merger(eng, dist):
+    """NativeMerger over RCCL; the torch-side TableMerger when the group is gloo."""
+    if dist.get_backend() == "nccl":
+        return NativeMerger(eng, dist)
+    return EpochMerger(eng, dist)
 
 
 def shard_heads(triples: np.ndarray, rank: int, world: int) -> np.ndarray:

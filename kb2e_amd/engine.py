@@ -27,8 +27,10 @@ EXPORTS = [
     "kb2e_synchronize", "kb2e_take_stats", "kb2e_rng_next", "kb2e_profile_enable", "kb2e_profile_query",
     "kb2e_device_bytes", "kb2e_device_tables", "kb2e_renormalize", "kb2e_evaluate", "kb2e_evaluate_transr_compat",
     "kb2e_renormalize_rows", "kb2e_init_params_device", "kb2e_write_table", "kb2e_format_table",
-    "kb2e_read_table",
+    "kb2e_read_table", "kb2e_comm_unique_id", "kb2e_comm_init_rank", "kb2e_comm_init_group", "kb2e_merge_epoch",
+    "kb2e_merge_epoch_group", "kb2e_comm_info",
 ]
+COMM_ID_BYTES = 128
 READ_VERBATIM, READ_UNIT, READ_SHRINK = 0, 1, 2
 
 
@@ -85,6 +87,12 @@ def lib():
             "kb2e_evaluate": (i32, [vp, i32p, i32p, i32p, i64, i32p, i32p, i32p, i64, dp]),
             "kb2e_evaluate_transr_compat": (i32, [vp, i32p, i32p, i32p, i64, i32p, i32p, i32p, i64, dp, dp, vp,
                                                   vp]),
+            "kb2e_comm_unique_id": (i32, [u8p]),
+            "kb2e_comm_init_rank": (i32, [vp, i32, i32, u8p]),
+            "kb2e_comm_init_group": (i32, [C.POINTER(vp), i32]),
+            "kb2e_merge_epoch": (i32, [vp]),
+            "kb2e_merge_epoch_group": (i32, [C.POINTER(vp), i32]),
+            "kb2e_comm_info": (i32, [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i64), C.POINTER(i64)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -230,6 +238,31 @@ class Engine:
                                                  count), "get_sample_stream")
         return si, sj, side
 
+    # ------------------------------------------------ multi-GPU epoch merge
+    @staticmethod
+    def comm_unique_id():
+        """A fresh RCCL id (bytes) for kb2e_comm_init_rank; made on one rank, handed to all."""
+        buf = (C.c_uint8 * COMM_ID_BYTES)()
+        st = lib().kb2e_comm_unique_id(buf)
+        if st != 0:
+            raise EngineError(f"kb2e_comm_unique_id failed: {STATUS.get(st, st)}")
+        return bytes(buf)
+
+    def comm_init_rank(self, nranks, rank, comm_id):
+        """Join the RCCL communicator (collective); rank 0's tables are broadcast."""
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(bytes(comm_id))
+        self._check(lib().kb2e_comm_init_rank(self.h, int(nranks), int(rank), buf), "comm_init_rank")
+
+    def merge_epoch(self):
+        """T <- renorm(T0 + sum_r (T_r - T0)) over the communicator (collective)."""
+        self._check(lib().kb2e_merge_epoch(self.h), "merge_epoch")
+
+    def comm_info(self):
+        n, r = C.c_int32(), C.c_int32()
+        lo, cnt = C.c_int64(), C.c_int64()
+        self._check(lib().kb2e_comm_info(self.h, C.byref(n), C.byref(r), C.byref(lo), C.byref(cnt)), "comm_info")
+        return n.value, r.value, lo.value, cnt.value
+
     def train_epoch(self):
         loss = C.c_double(0)
         act = C.c_int64(0)
@@ -299,3 +332,22 @@ class Engine:
 
     def device_bytes(self):
         return lib().kb2e_device_bytes(self.h)
+
+
+def _handles(engines):
+    arr = (C.c_void_p * len(engines))(*[e.h for e in engines])
+    return arr
+
+
+def comm_init_group(engines):
+    """One host thread driving every engine (kb2e_comm_init_group): RCCL over the
+    engines' devices, or the local kernel backend when they share a device."""
+    st = lib().kb2e_comm_init_group(_handles(engines), len(engines))
+    if st != 0:
+        raise EngineError(f"comm_init_group: {STATUS.get(st, st)}: {lib().kb2e_last_error(engines[0].h).decode()}")
+
+
+def merge_epoch_group(engines):
+    st = lib().kb2e_merge_epoch_group(_handles(engines), len(engines))
+    if st != 0:
+        raise EngineError(f"merge_epoch_group: {STATUS.get(st, st)}: {lib().kb2e_last_error(engines[0].h).decode()}")

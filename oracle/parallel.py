@@ -75,7 +75,7 @@ def transe_parallel_batches(ent, rel, triples, si, sj, side, B, nbatches, *, rat
 
 
 def transr_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, rate, margin=1.0, l1=True,
-                            compat=False, work=None, St=32, constraint=True):
+                            compat=False, work=None, St=32, constraint=True, renorm="none", stats=None):
     """Train `nbatches` TransR batches of the PARALLEL schedule in place
     (kb2e_amd/csrc/kernels_transr_parallel.hpp).  Returns (loss, active).
 
@@ -140,11 +140,12 @@ def transr_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
         ent[ea] += acc[ea]
         ent[ea] /= np.sqrt((ent[ea] ** 2).sum(1, keepdims=True))
         if constraint:
-            transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St)
+            transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St, renorm=renorm, stats=stats)
     return loss, active
 
 
-def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, relpair=True, max_iter=256):
+def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, relpair=True, max_iter=256,
+                      renorm="none", stats=None):
     """transRNorm step of the PARALLEL TransR schedule, in place.
 
     Per relation of the batch: pairs (h', r), (t', r) of the active updates in
@@ -155,20 +156,150 @@ def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, 
     the loop in Jacobi form to first order, iterated on the projection
     p = W^T a: p <- p - 2 lr W^T W p - 2 lr |a0|^2 p, G += 2 p while |p|^2 > 1,
     then da = -lr W G, dW = -lr a0 G^T (kernels_transr_mfma.hpp).
+
+    renorm (experiment): "none" = the corrections are added after the batch's
+    unit norms; "all" = the touched W rows and corrected entity rows are scaled
+    back to unit length after the corrections; "last" = every correction except
+    those of the row's last update in the batch (the reference re-normalises a
+    row at each later update, transr/trainer.cpp:174-180) is added before a
+    unit norm, the last update's after it.
     """
     ra = np.unique(r[act])
+    if renorm.startswith("seq"):  # experiment: the reference's loop, pairs in order per relation (Gauss-Seidel)
+        from oracle import orc
+        for rr in ra:
+            slots = []
+            for kk in np.nonzero((r == rr) & act)[0]:
+                slots += [h[kk], t[kk], rr, nh[kk], nt[kk], rr] if relpair else [h[kk], t[kk], nh[kk], nt[kk]]
+            seen = set()
+            Wm = W[rr].copy()
+            nf = 0
+            for e in slots:
+                if e >= ent.shape[0] or (renorm == "seq" and e in seen):
+                    continue
+                seen.add(e)
+                if stats is not None:
+                    pp = Wm.T @ ent[e]
+                    nf += int(pp @ pp > 1.0)
+                ent[e], Wm = orc.transr_norm(ent[e], Wm, rate)
+            W[rr] = Wm
+            if stats is not None:
+                stats["pairs"] = stats.get("pairs", 0) + len(seen)
+                stats["fired"] = stats.get("fired", 0) + nf
+                stats["max_rel_pairs"] = max(stats.get("max_rel_pairs", 0), len(seen))
+                stats["max_rel_fired"] = max(stats.get("max_rel_fired", 0), nf)
+        return
+    if renorm.startswith("jc"):  # experiment: Jacobi within chunks of C pairs, Gauss-Seidel across chunks
+        C = int(renorm[2:])
+        W0 = W.copy()
+        E1 = ent.copy()
+        dE = np.zeros_like(ent)
+        for rr in ra:
+            slots = []
+            for kk in np.nonzero((r == rr) & act)[0]:
+                slots += [h[kk], t[kk], nh[kk], nt[kk]]
+            if relpair and rr < ent.shape[0]:
+                slots.append(rr)
+            seen, uniq = set(), []
+            for e in slots:
+                if e not in seen:
+                    seen.add(e)
+                    uniq.append(e)
+            Wm = W0[rr]
+            K0 = Wm.T @ Wm
+            Wc = Wm.copy()
+            for c0 in range(0, len(uniq), C):
+                A = E1[uniq[c0:c0 + C]]
+                P = A @ Wc                     # rows p_k = Wc^T a_k
+                Q0 = (P * P).sum(1)
+                dWc = np.zeros_like(Wc)
+                for k in np.nonzero(Q0 > 1.0)[0]:
+                    p, a0 = P[k], A[k]
+                    s0 = a0 @ a0
+                    v = K0 @ p + s0 * p
+                    d, ee = p @ v, v @ v
+                    m = 0
+                    while m < max_iter:
+                        q = Q0[k] - 4 * rate * m * d + 4 * rate * rate * m * m * ee
+                        if not q > 1.0:
+                            break
+                        m += 1
+                    G = 2.0 * m * p - 2.0 * rate * m * (m - 1) * v
+                    dWc -= rate * np.outer(a0, G)
+                    dE[uniq[c0 + k]] += -rate * (Wm @ G)
+                    if stats is not None:
+                        stats["fired"] = stats.get("fired", 0) + 1
+                Wc = Wc + dWc
+            W[rr] = Wc
+        ent += dE
+        return
+    if renorm == "gs1":  # experiment: first-order Gauss-Seidel over the relation's pairs (closed-form rounds)
+        W0 = W.copy()
+        E1 = ent.copy()
+        dE = np.zeros_like(ent)
+        for rr in ra:
+            slots = []
+            for kk in np.nonzero((r == rr) & act)[0]:
+                slots += [h[kk], t[kk], nh[kk], nt[kk]]
+            if relpair and rr < ent.shape[0]:
+                slots.append(rr)
+            Wm = W0[rr]
+            K0 = Wm.T @ Wm
+            Wc = Wm.copy()
+            seen = set()
+            for e in slots:
+                if e in seen:
+                    continue
+                seen.add(e)
+                a0 = E1[e]
+                s0 = a0 @ a0
+                p = Wc.T @ a0
+                Q0 = p @ p
+                if not Q0 > 1.0:
+                    if stats is not None:
+                        stats["pairs"] = stats.get("pairs", 0) + 1
+                    continue
+                v = K0 @ p + s0 * p
+                d, ee = p @ v, v @ v
+                m = 0
+                while m < max_iter:  # |p_m|^2 with p_m = p - 2 lr m v (first order in lr)
+                    q = Q0 - 4 * rate * m * d + 4 * rate * rate * m * m * ee
+                    if not q > 1.0:
+                        break
+                    m += 1
+                G = 2.0 * m * p - 2.0 * rate * m * (m - 1) * v
+                Wc = Wc - rate * np.outer(a0, G)
+                dE[e] += -rate * (Wm @ G)
+                if stats is not None:
+                    stats["pairs"] = stats.get("pairs", 0) + 1
+                    stats["fired"] = stats.get("fired", 0) + 1
+                    stats["rounds"] = stats.get("rounds", 0) + m
+            W[rr] = Wc
+        ent += dE
+        return
     W0 = W.copy()
     E1 = ent.copy()
     dWc = np.zeros_like(W)
+    dWl = np.zeros_like(W)   # the corrections of each relation's last update
+    dE = np.zeros_like(ent)
+    dEl = np.zeros_like(ent)
+    # the last update touching each entity: (sample, update) order key
+    last_key = {}
+    for kk in np.nonzero(act)[0]:
+        for u, (hh, tt) in enumerate(((h[kk], t[kk]), (nh[kk], nt[kk]))):
+            for e in (hh, tt):
+                last_key[e] = (kk, u)
     for rr in ra:
         slots = []
-        for kk in np.nonzero(r == rr)[0]:
-            for (hh, tt) in ((h[kk], t[kk]), (nh[kk], nt[kk])):
-                slots += [hh, tt] if act[kk] else [-1, -1]
+        ks = np.nonzero(r == rr)[0]
+        last_act = ks[act[ks]][-1]
+        for kk in ks:
+            for u, (hh, tt) in enumerate(((h[kk], t[kk]), (nh[kk], nt[kk]))):
+                slots += [(hh, kk, u), (tt, kk, u)] if act[kk] else [(-1, kk, u), (-1, kk, u)]
         if relpair and rr < ent.shape[0]:
-            slots.append(rr)
+            slots.append((rr, last_act, 1))
         seen = set()
-        for e in slots:
+        for (e, kk, u) in slots:
             if e < 0 or (dedupe and e in seen):
                 continue
             seen.add(e)
@@ -177,14 +308,33 @@ def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, 
             G = np.zeros_like(a0)
             s0 = a0 @ a0
             p = Wm.T @ a0
+            it = 0
             for _ in range(max_iter):
                 if not (p @ p > 1.0):
                     break
                 G += 2.0 * p
                 p = p - 2.0 * rate * (Wm.T @ (Wm @ p)) - 2.0 * rate * s0 * p
-            ent[e] += -rate * (Wm @ G)
-            dWc[rr] += np.outer(-rate * a0, G)
+                it += 1
+            if stats is not None:
+                stats["pairs"] = stats.get("pairs", 0) + 1
+                stats["fired"] = stats.get("fired", 0) + (it > 0)
+            if not it:
+                continue
+            # "last": a correction made before the row's last update in the batch is
+            # followed, in the reference, by that update's unit norm; the last
+            # update's own corrections persist
+            rel_post = renorm == "none" or (renorm == "last" and (kk, u) >= (last_act, 1))
+            ent_post = renorm == "none" or e not in last_key or (renorm == "last" and (kk, u) >= last_key[e])
+            (dEl if ent_post else dE)[e] += -rate * (Wm @ G)
+            (dWl if rel_post else dWc)[rr] += np.outer(-rate * a0, G)
     W[ra] += dWc[ra]
+    if renorm != "none":
+        W[ra] /= np.sqrt((W[ra] ** 2).sum(2, keepdims=True))
+    W[ra] += dWl[ra]
+    ec = np.nonzero(np.any(dE != 0, axis=1))[0]
+    ent[ec] += dE[ec]
+    ent[ec] /= np.sqrt((ent[ec] ** 2).sum(1, keepdims=True))
+    ent += dEl
 
 
 def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, rate, margin=1.0):

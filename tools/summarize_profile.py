@@ -48,13 +48,17 @@ def phase(name):
     return None
 
 
+CLOCK_HZ, SIMDS, XCDS = 2.4e9, 1024, 8  # MI355X_MICROARCH.md: 256 CUs x 4 SIMDs in 8 XCDs
 PEAK_F64_MFMA_TFLOPS = 78.6  # v_mfma_f64_16x16x4_f64: 64 cycles / 2048 FLOP per SIMD, 1024 SIMDs, 2.4 GHz
 
 
 def mfma_table(src, stats):
     """f64 MFMA work and utilisation per kernel from the SQ_INSTS_VALU_MFMA_MOPS_F64
     / SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE pass (rocprofv3 derived-counter
-    formulas: MfmaFlopsF64 = MOPS_F64 x 512, MfmaUtil = BUSY / (GUI_ACTIVE x SIMDs))."""
+    formulas: MfmaFlopsF64 = MOPS_F64 x 512).  SQ_VALU_MFMA_BUSY_CYCLES is summed over
+    all 1024 SIMDs and GRBM_GUI_ACTIVE over the 8 XCDs, so the utilisation is
+    BUSY / (kernel cycles x 1024 SIMDs) with kernel cycles = the rocprofv3 average
+    duration x 2.4 GHz (mfma_util_pct) or GUI_ACTIVE / 8 (mfma_util_pct_gui)."""
     path = os.path.join(src, "pmc_MFMA", "run_counter_collection.csv")
     if not os.path.exists(path):
         return {}
@@ -79,7 +83,8 @@ def mfma_table(src, stats):
                   "achieved_tflops": flops / (us * 1e-6) / 1e12 if us else None,
                   "frac_of_f64_mfma_peak": (flops / (us * 1e-6) / 1e12) / PEAK_F64_MFMA_TFLOPS if us else None,
                   "mfma_busy_cycles": busy, "gui_active_cycles": gui,
-                  "mfma_util_pct": 100.0 * busy / (gui * 1024) if gui else None}
+                  "mfma_util_pct": 100.0 * busy / (us * 1e-6 * CLOCK_HZ * SIMDS) if us else None,
+                  "mfma_util_pct_gui": 100.0 * busy / (gui / XCDS * SIMDS) if gui else None}
     return out
 
 
@@ -137,11 +142,12 @@ def main(src, tag, config, prec, schedule="parallel", batches="200"):
         lines.append(f"| {fam} | {v['fetch_bytes_raw']:.0f} | {v['write_bytes']:.0f} | {v['hbm_bytes_per_launch']:.0f} |")
     if mf:
         lines += ["", f"## f64 MFMA per launch (PMC: SQ_INSTS_VALU_MFMA_MOPS_F64 x 512; peak {PEAK_F64_MFMA_TFLOPS} TF)", "",
-                  "| kernel | MFMA FLOP | avg us | TFLOP/s | frac of f64 MFMA peak | MfmaUtil % |", "|---|---|---|---|---|---|"]
+                  "| kernel | MFMA FLOP | avg us | TFLOP/s | frac of f64 MFMA peak | MfmaUtil % (duration) | MfmaUtil % (GUI_ACTIVE/8) |",
+                  "|---|---|---|---|---|---|---|"]
         for k, v in sorted(mf.items(), key=lambda kv: -kv[1]["mfma_f64_flop_per_launch"]):
             lines.append(f"| {k[:50]} | {v['mfma_f64_flop_per_launch']:.3g} | {v['avg_us'] or 0:.1f} | "
                          f"{v['achieved_tflops'] or 0:.2f} | {v['frac_of_f64_mfma_peak'] or 0:.4f} | "
-                         f"{v['mfma_util_pct'] or 0:.2f} |")
+                         f"{v['mfma_util_pct'] or 0:.2f} | {v['mfma_util_pct_gui'] or 0:.2f} |")
     md = os.path.join(root, "profiles", f"{tag}_{config}_{schedule}_f{prec}.md")
     open(md, "w").write("\n".join(lines) + "\n")
     print(md, out_json)
