@@ -172,6 +172,7 @@ struct RParBufs {
     int32_t* cpairs;     // [tiles][2][kCPairs]
     int32_t* cnrows;     // [tiles]
     int32_t stats;       // count transRNorm rounds (tools)
+    int32_t last_renorm; // transRNorm pass: entity rows renormalised between pre / post pair deltas (kernels_transr_seq.hpp)
     int32_t dbg;         // transRNorm wave kernel: phases skipped for timing experiments (tools; wrong results)
 };
 
@@ -704,23 +705,51 @@ __global__ __launch_bounds__(256) void transr_constraint_kernel(RParArgs a, RPar
 // 1024-thread workgroup).  GRAD: head role -beta lr y, tail role +beta lr y
 // (transr/trainer.cpp:168-169), then the unit norm (:175-176) if an active
 // update used the row as head or tail.  !GRAD: the transRNorm pair deltas
-// (and the (entity[r], r) delta once), no norm.
+// (and the (entity[r], r) delta once), no norm -- or, with bf.last_renorm (the
+// per-relation chunk kernel, kernels_transr_seq.hpp), the deltas of pairs made
+// before the row's last update of the batch ("pre": the reference's unit norm
+// at that update follows them), a unit norm, then the deltas of the last
+// update's own pairs ("post"; the (entity[r], r) delta is post when no update
+// touches the row as head or tail, pre otherwise).
 constexpr int kRParWaves = 16;
+
+// The row's last active update in the batch, kk 2 + u (-1: none), over the
+// events [p0 + 64 first, ...) of its segment in strides of 64 stride; the
+// maximum in every lane.
+__device__ __forceinline__ int rpar_entity_last(const RParArgs& a, int p0, int p1, int first, int stride) {
+    const int l = lane_id();
+    int last = -1;
+    for (int base = p0 + first * kWave; base < p1; base += stride * kWave) {
+        const int p = base + l;
+        if (p < p1) {
+            const uint64_t key = a.keys[p];
+            const int kk = a.kl.kk_of(key);
+            if (a.act[kk] && (key & (kRoleHead | kRoleTail))) last = max(last, kk * 2 + (int)((key >> 3) & 1));
+        }
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) last = max(last, __shfl_xor(last, s));
+    return last;
+}
 
 // Events [p0 + 64 first, ...) of an entity segment in chunks of 64 (lane q:
 // event q); the rows the active ones add (y rows, or transRNorm pair deltas)
 // are then fetched four at a time, so a long segment keeps several loads in
-// flight instead of one dependent chain per event.
+// flight instead of one dependent chain per event.  acc / dirty: the deltas
+// (GRAD, and !GRAD without last_renorm: all of them; with it: the pre ones),
+// acc2 / dirty2: the post ones of update `last`.
 template <typename T, bool GRAD>
 __device__ __forceinline__ void rpar_entity_events(const RParArgs& a, const RParBufs<T>& bf, int row, int p0, int p1,
-                                                   int first, int stride, T (&acc)[2], bool& dirty, bool& er_seen) {
+                                                   int first, int stride, int last, T (&acc)[2], T (&acc2)[2],
+                                                   bool& dirty, bool& dirty2, bool& er_seen) {
     const int n = a.n, ld = a.ld, l = lane_id();
+    const bool split = !GRAD && bf.last_renorm;
     for (int base = p0 + first * kWave; base < p1; base += stride * kWave) {
         const int p = base + l;
         int src = -1;     // row of the y / pair table this lane's event adds (GRAD: its y row)
         int src2 = -1;    // !GRAD: second pair row (the row is head and tail of the update)
         T c = T(0);
-        bool nrm = false, er = false;
+        bool nrm = false, er = false, post = false;
         if (p < p1) {
             const uint64_t key = a.keys[p];
             const int kk = a.kl.kk_of(key);
@@ -740,6 +769,7 @@ __device__ __forceinline__ void rpar_entity_events(const RParArgs& a, const RPar
                     const bool ph = hd && (!bf.pflag || bf.pflag[s0]);
                     const bool pt = tl && (!bf.pflag || bf.pflag[s0 + 1]);
                     nrm = ph || pt;
+                    post = split && kk * 2 + u == last;
                     if (ph) src = s0;
                     if (pt) {
                         if (src < 0) src = s0 + 1;
@@ -748,12 +778,14 @@ __device__ __forceinline__ void rpar_entity_events(const RParArgs& a, const RPar
                 }
             }
         }
-        if (__ballot(nrm)) dirty = true;
+        if (__ballot(nrm && !post)) dirty = true;
+        if (__ballot(nrm && post)) dirty2 = true;
         if (__ballot(er)) er_seen = true;
         const T* tab = GRAD ? bf.y : bf.pair;
         for (int pass = 0; pass < (GRAD ? 1 : 2); ++pass) {
             const int mine = pass ? src2 : src;
             uint64_t m = __ballot(mine >= 0);
+            const uint64_t pm = __ballot(post);
             while (m) {
                 int ev[4];
                 int k = 0;
@@ -769,8 +801,9 @@ __device__ __forceinline__ void rpar_entity_events(const RParArgs& a, const RPar
                 for (int q = 0; q < 4; ++q)
                     if (q < k) {
                         const T cq = GRAD ? readlane_f(c, ev[q]) : T(1);
-                        acc[0] += cq * v[q][0];
-                        acc[1] += cq * v[q][1];
+                        T(&dst)[2] = ((pm >> ev[q]) & 1) ? acc2 : acc;
+                        dst[0] += cq * v[q][0];
+                        dst[1] += cq * v[q][1];
                     }
             }
         }
@@ -779,25 +812,38 @@ __device__ __forceinline__ void rpar_entity_events(const RParArgs& a, const RPar
 
 template <typename T, bool GRAD>
 __device__ __forceinline__ void rpar_entity_finish(const RParArgs& a, const RParBufs<T>& bf, int row, T (&acc)[2],
-                                                   bool dirty, bool er_seen) {
+                                                   T (&acc2)[2], bool dirty, bool dirty2, bool er_seen, int last) {
     const int n = a.n, ld = a.ld;
+    const bool split = !GRAD && bf.last_renorm;
     if (!GRAD && er_seen && row < a.nr && bf.relpair_stamp[row] == bf.stamp) {
         T dv[2];
         lane_pair_load(bf.relpair + (int64_t)row * ld, n, dv);
-        acc[0] += dv[0];
-        acc[1] += dv[1];
-        dirty = true;
+        if (split && last < 0) {  // no update renormalises the row: the delta stays
+            acc2[0] += dv[0];
+            acc2[1] += dv[1];
+            dirty2 = true;
+        } else {
+            acc[0] += dv[0];
+            acc[1] += dv[1];
+            dirty = true;
+        }
     }
-    if (!dirty) return;
+    if (!dirty && !dirty2) return;
     T* ptr = bf.ent + (int64_t)row * ld;
     T v[2];
     lane_pair_load(ptr, n, v);
-    v[0] += acc[0];
-    v[1] += acc[1];
-    if (GRAD) {
+    if (dirty) {
+        v[0] += acc[0];
+        v[1] += acc[1];
+    }
+    if (GRAD || (split && dirty)) {
         const T len = sqrt(wave_sum(v[0] * v[0] + v[1] * v[1]));
         v[0] = v[0] / len;
         v[1] = v[1] / len;
+    }
+    if (dirty2) {
+        v[0] += acc2[0];
+        v[1] += acc2[1];
     }
     lane_pair_store(ptr, n, v);
 }
@@ -805,10 +851,11 @@ __device__ __forceinline__ void rpar_entity_finish(const RParArgs& a, const RPar
 // the entity rows of workgroup `bid` of G (1024 threads)
 template <typename T, bool GRAD>
 __device__ __forceinline__ void transr_entity_block(RParArgs a, RParBufs<T> bf, int32_t long_min, int bid, int G) {
-    __shared__ T part[kRParWaves][2][kWave];
-    __shared__ int flags[2];
+    __shared__ T part[kRParWaves][4][kWave];
+    __shared__ int flags[4];
     __shared__ int longs[1024], nlong;
     const int w = threadIdx.x >> 6, l = lane_id();
+    const bool split = !GRAD && bf.last_renorm;
     const int s0 = a.batch_seg[a.batch], s1 = a.rel_begin[a.batch];  // entity segments sort first
     const int blockIdx_x = bid;
     // long segments: whole workgroup, segments s0 + blockIdx_x, s0 + blockIdx_x + G, ... that are
@@ -825,24 +872,39 @@ __device__ __forceinline__ void transr_entity_block(RParArgs a, RParBufs<T> bf, 
         const int s = longs[li];
         const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
         const int row = a.seg_row[s];
-        if (threadIdx.x < 2) flags[threadIdx.x] = 0;
+        if (threadIdx.x < 4) flags[threadIdx.x] = threadIdx.x == 3 ? -1 : 0;
         __syncthreads();
-        T acc[2] = {T(0), T(0)};
-        bool dirty = false, er = false;
-        rpar_entity_events<T, GRAD>(a, bf, row, p0, p1, w, kRParWaves, acc, dirty, er);  // chunks w, w + 16, ...
+        int last = -1;
+        if (split) {  // the row's last update over the whole segment (chunks w, w + 16, ...)
+            last = rpar_entity_last(a, p0, p1, w, kRParWaves);
+            if (l == 0) atomicMax(&flags[3], last);
+            __syncthreads();
+            last = flags[3];
+        }
+        T acc[2] = {T(0), T(0)}, acc2[2] = {T(0), T(0)};
+        bool dirty = false, dirty2 = false, er = false;
+        rpar_entity_events<T, GRAD>(a, bf, row, p0, p1, w, kRParWaves, last, acc, acc2, dirty, dirty2,
+                                    er);  // chunks w, w + 16, ...
         part[w][0][l] = acc[0];
         part[w][1][l] = acc[1];
+        part[w][2][l] = acc2[0];
+        part[w][3][l] = acc2[1];
         if (l == 0 && dirty) atomicOr(&flags[0], 1);
         if (l == 0 && er) atomicOr(&flags[1], 1);
+        if (l == 0 && dirty2) atomicOr(&flags[2], 1);
         __syncthreads();
         if (w == 0) {
             acc[0] = part[0][0][l];
             acc[1] = part[0][1][l];
+            acc2[0] = part[0][2][l];
+            acc2[1] = part[0][3][l];
             for (int v = 1; v < kRParWaves; ++v) {
                 acc[0] += part[v][0][l];
                 acc[1] += part[v][1][l];
+                acc2[0] += part[v][2][l];
+                acc2[1] += part[v][3][l];
             }
-            rpar_entity_finish<T, GRAD>(a, bf, row, acc, flags[0] != 0, flags[1] != 0);
+            rpar_entity_finish<T, GRAD>(a, bf, row, acc, acc2, flags[0] != 0, flags[2] != 0, flags[1] != 0, last);
         }
         __syncthreads();
         }
@@ -852,10 +914,11 @@ __device__ __forceinline__ void transr_entity_block(RParArgs a, RParBufs<T> bf, 
         const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
         if (p1 - p0 >= long_min) continue;
         const int row = a.seg_row[s];
-        T acc[2] = {T(0), T(0)};
-        bool dirty = false, er = false;
-        rpar_entity_events<T, GRAD>(a, bf, row, p0, p1, 0, 1, acc, dirty, er);
-        rpar_entity_finish<T, GRAD>(a, bf, row, acc, dirty, er);
+        const int last = split ? rpar_entity_last(a, p0, p1, 0, 1) : -1;
+        T acc[2] = {T(0), T(0)}, acc2[2] = {T(0), T(0)};
+        bool dirty = false, dirty2 = false, er = false;
+        rpar_entity_events<T, GRAD>(a, bf, row, p0, p1, 0, 1, last, acc, acc2, dirty, dirty2, er);
+        rpar_entity_finish<T, GRAD>(a, bf, row, acc, acc2, dirty, dirty2, er, last);
     }
 }
 

@@ -10,6 +10,7 @@
 
 #include "hip_util.hpp"
 #include "kernels_transr_cons.hpp"
+#include "kernels_transr_seq.hpp"
 #include "kernels_transr_wave.hpp"
 
 namespace kb2e {
@@ -42,7 +43,41 @@ const void* cons_fn(int n) {
     return kernel_fn<T>(kCons, n);
 }
 
+template <typename T, int C>
+const void* seq_fn(int n) {
+    switch (rm_np(n)) {
+        case 16: return (const void*)transr_cons_seq_kernel<T, 16, C>;
+        case 32: return (const void*)transr_cons_seq_kernel<T, 32, C>;
+        case 48: return (const void*)transr_cons_seq_kernel<T, 48, C>;
+        case 64: return (const void*)transr_cons_seq_kernel<T, 64, C>;
+    }
+    throw std::runtime_error("transRNorm chunk kernel: n > 64");
+}
+
+template <typename T>
+const void* seq_fn(int n, int C) {
+    return C == 64 ? seq_fn<T, 64>(n) : C == 16 ? seq_fn<T, 16>(n) : seq_fn<T, 32>(n);
+}
+
 }  // namespace
+
+size_t cons_seq_setup(int n, int C, int esize) {
+    const size_t lds = esize == 8 ? seq_lds<double>(n, C) : seq_lds<float>(n, C);
+    HIPCHK(hipFuncSetAttribute(esize == 8 ? seq_fn<double>(n, C) : seq_fn<float>(n, C),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    return lds;
+}
+
+template <typename T>
+void cons_seq_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, int C, size_t lds, hipStream_t stream) {
+    RParArgs aa = a;
+    RParBufs<T> bb = bf;
+    void* args[] = {&aa, &bb};
+    HIPCHK(hipLaunchKernel(seq_fn<T>(a.n, C), dim3(grid), dim3(kSeqThreads), args, lds, stream));
+}
+
+template void cons_seq_launch<double>(const RParArgs&, const RParBufs<double>&, int, int, size_t, hipStream_t);
+template void cons_seq_launch<float>(const RParArgs&, const RParBufs<float>&, int, int, size_t, hipStream_t);
 
 bool cons_wave_supported(int n) { return n >= 1 && n <= 64; }
 
@@ -86,6 +121,12 @@ template void grad_wave_launch<float>(const RParArgs&, const RParBufs<float>&, i
 
 template void cons_wave_launch<double>(const RParArgs&, const RParBufs<double>&, int, size_t, hipStream_t);
 template void cons_wave_launch<float>(const RParArgs&, const RParBufs<float>&, int, size_t, hipStream_t);
+
+void cons_seq_take_stats(unsigned long long (&st)[8]) {
+    HIPCHK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_seq_stats), sizeof(st)));
+    unsigned long long z[8] = {};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_seq_stats), z, sizeof(z)));
+}
 
 void cons_wave_take_stats(unsigned long long (&st)[16]) {
     unsigned long long mine[16];

@@ -75,7 +75,7 @@ def transe_parallel_batches(ent, rel, triples, si, sj, side, B, nbatches, *, rat
 
 
 def transr_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, rate, margin=1.0, l1=True,
-                            compat=False, work=None, St=32, constraint=True, renorm="none", stats=None):
+                            compat=False, work=None, St=32, constraint=True, cons="jacobi", stats=None):
     """Train `nbatches` TransR batches of the PARALLEL schedule in place
     (kb2e_amd/csrc/kernels_transr_parallel.hpp).  Returns (loss, active).
 
@@ -83,9 +83,9 @@ def transr_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
     projections, energies (compat: the reference's accumulating work vectors,
     transr/transr.cpp:20-25, carried in `work` = [head, tail]), hinge, x, d =
     h - t, y = W x; summed dW, dr per relation, summed entity deltas; unit
-    norms; then one Jacobi step of transRNorm (transr/trainer.cpp:35-64) on
-    every (h', r), (t', r) pair of an active update and (entity'[r], r) once per
-    relation, iterated while |W^T a|^2 > 1, per tile of St samples.
+    norms; then transRNorm (transr/trainer.cpp:35-64) on every (h', r), (t', r)
+    pair of an active update and (entity'[r], r) once per relation, iterated
+    while |W^T a|^2 > 1 (transr_constraint: `cons` picks the kernel's form).
     """
     loss = 0.0
     active = 0
@@ -140,169 +140,170 @@ def transr_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
         ent[ea] += acc[ea]
         ent[ea] /= np.sqrt((ent[ea] ** 2).sum(1, keepdims=True))
         if constraint:
-            transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St, renorm=renorm, stats=stats)
+            transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St, cons=cons, stats=stats)
     return loss, active
 
 
+def _relation_pairs(r, rr, act, h, t, nh, nt, relpair, ne):
+    """The transRNorm pairs of relation rr in the batch: the (h', r), (t', r)
+    entities of its active updates in (sample, update, role) order, then
+    (entity'[r], r) (transr/trainer.cpp:185-187); first occurrences only."""
+    slots = []
+    for kk in np.nonzero((r == rr) & act)[0]:
+        slots += [h[kk], t[kk], nh[kk], nt[kk]]
+    if relpair and rr < ne:
+        slots.append(rr)
+    seen, uniq = set(), []
+    for e in slots:
+        if e not in seen:
+            seen.add(e)
+            uniq.append(int(e))
+    return uniq
+
+
+def _relation_items(r, rr, act, h, t, nh, nt, relpair, ne):
+    """_relation_pairs with each pair's update: (entity, (sample, update)), the
+    (entity'[r], r) pair last as (r, None)."""
+    items, seen = [], set()
+    for kk in np.nonzero((r == rr) & act)[0]:
+        for u, (hh, tt) in enumerate(((h[kk], t[kk]), (nh[kk], nt[kk]))):
+            for e in (int(hh), int(tt)):
+                if e not in seen:
+                    seen.add(e)
+                    items.append((e, (int(kk), u)))
+    if relpair and rr < ne and int(rr) not in seen:
+        items.append((int(rr), None))
+    return items
+
+
+def transr_norm_rounds(p, a0, K0, Q0, eps, max_iter=256):
+    """transRNorm's loop (transr/trainer.cpp:35-64) on the projection p = W^T a:
+    p_{t+1} = p_t - eps (K0 + |a|^2) p_t, G = sum of 2 p_t over the rounds t < m
+    while |p_t|^2 > 1.  With v = (K0 + |a|^2) p = kappa p + w (w orthogonal to
+    p) and rho = 1 - eps kappa: p_t = rho^t p - eps t rho^(t-1) w to first order
+    in eps along w (exact for m <= 2, geometric for long runs), so
+    |p_t|^2 = rho^2t Q0 + eps^2 t^2 rho^(2t-2) |w|^2 and
+    G = 2 (S0 p - eps S1 w), S0 = sum rho^t, S1 = sum t rho^(t-1).  Returns (G, m)."""
+    v = K0 @ p + (a0 @ a0) * p
+    kappa = (p @ v) / Q0
+    w = v - kappa * p
+    w2 = w @ w
+    rho = 1.0 - eps * kappa
+    m, S0, S1, rt, rtm1 = 0, 0.0, 0.0, 1.0, 0.0  # rt = rho^t, rtm1 = rho^(t-1) (0 at t = 0)
+    while m < max_iter and rt * rt * Q0 + eps * eps * m * m * rtm1 * rtm1 * w2 > 1.0:
+        S0 += rt
+        S1 += m * rtm1
+        m += 1
+        rtm1 = rt
+        rt *= rho
+    return 2.0 * (S0 * p - eps * S1 * w), m
+
+
 def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, relpair=True, max_iter=256,
-                      renorm="none", stats=None):
+                      cons="jacobi", stats=None):
     """transRNorm step of the PARALLEL TransR schedule, in place.
 
-    Per relation of the batch: pairs (h', r), (t', r) of the active updates in
-    (sample, update, role) order, then (entity'[r], r) (transr/trainer.cpp:187);
-    first occurrences per relation only (the GPU's per-batch (relation, entity)
-    table, kernels_transr_parallel.hpp transr_pair_dup: independent of how the
-    relation is cut into tiles, so St is unused);
-    the loop in Jacobi form to first order, iterated on the projection
-    p = W^T a: p <- p - 2 lr W^T W p - 2 lr |a0|^2 p, G += 2 p while |p|^2 > 1,
-    then da = -lr W G, dW = -lr a0 G^T (kernels_transr_mfma.hpp).
+    cons = "jacobi" (kernels_transr_mfma.hpp / kernels_transr_parallel.hpp tile
+    kernels): per relation of the batch, pairs (h', r), (t', r) of the active
+    updates in (sample, update, role) order, then (entity'[r], r)
+    (transr/trainer.cpp:187); first occurrences per relation only (the GPU's
+    per-batch (relation, entity) table, kernels_transr_parallel.hpp
+    transr_pair_dup: independent of how the relation is cut into tiles, so St is
+    unused); every pair against the same W' (Jacobi), the loop iterated on the
+    projection p = W^T a: p <- p - 2 lr W^T W p - 2 lr |a0|^2 p, G += 2 p while
+    |p|^2 > 1, then da = -lr W G, dW = -lr a0 G^T, all summed.
 
-    renorm (experiment): "none" = the corrections are added after the batch's
-    unit norms; "all" = the touched W rows and corrected entity rows are scaled
-    back to unit length after the corrections; "last" = every correction except
-    those of the row's last update in the batch (the reference re-normalises a
-    row at each later update, transr/trainer.cpp:174-180) is added before a
-    unit norm, the last update's after it.
+    cons = "chunk<C>" (kernels_transr_seq.hpp, the default for n <= 64): the
+    same pairs of a relation walked in order, C at a time; inside a chunk every
+    pair against the chunk's W_c (Jacobi), and W_c takes the chunk's
+    corrections before the next chunk (Gauss-Seidel across chunks, as the
+    reference's successive calls see each other's shrinks).  The pairs of the
+    relation's last update (the corrupted triple of its last active sample) and
+    (entity'[r], r) form the final chunk, after W_c's rows are renormalised
+    (the reference renormalises W' at every update, so only the last update's
+    shrinks outlive the batch); likewise an entity's corrections from pairs
+    before its own last update are followed by a unit norm, those of its last
+    update (or of (entity'[r], r) when no update touches the row) are not.
+    Per violator the rounds in closed form (transr_norm_rounds, K0 = W'^T W');
+    da = -lr W_c G, W_c -= lr a G^T.
+
+    cons = "seq" (probe only, tools/probe_compat_parallel.py): the reference's
+    own loop (oracle/orc.c transr_norm) on each pair in order, on the evolving
+    matrix.
     """
     ra = np.unique(r[act])
-    if renorm.startswith("seq"):  # experiment: the reference's loop, pairs in order per relation (Gauss-Seidel)
+    ne = ent.shape[0]
+    if cons == "seq":
         from oracle import orc
         for rr in ra:
-            slots = []
-            for kk in np.nonzero((r == rr) & act)[0]:
-                slots += [h[kk], t[kk], rr, nh[kk], nt[kk], rr] if relpair else [h[kk], t[kk], nh[kk], nt[kk]]
-            seen = set()
             Wm = W[rr].copy()
             nf = 0
-            for e in slots:
-                if e >= ent.shape[0] or (renorm == "seq" and e in seen):
-                    continue
-                seen.add(e)
+            pairs = _relation_pairs(r, rr, act, h, t, nh, nt, relpair, ne)
+            for e in pairs:
                 if stats is not None:
                     pp = Wm.T @ ent[e]
                     nf += int(pp @ pp > 1.0)
                 ent[e], Wm = orc.transr_norm(ent[e], Wm, rate)
             W[rr] = Wm
             if stats is not None:
-                stats["pairs"] = stats.get("pairs", 0) + len(seen)
+                stats["pairs"] = stats.get("pairs", 0) + len(pairs)
                 stats["fired"] = stats.get("fired", 0) + nf
-                stats["max_rel_pairs"] = max(stats.get("max_rel_pairs", 0), len(seen))
-                stats["max_rel_fired"] = max(stats.get("max_rel_fired", 0), nf)
-        return
-    if renorm.startswith("jc"):  # experiment: Jacobi within chunks of C pairs, Gauss-Seidel across chunks
-        C = int(renorm[2:])
-        W0 = W.copy()
-        E1 = ent.copy()
-        dE = np.zeros_like(ent)
-        for rr in ra:
-            slots = []
-            for kk in np.nonzero((r == rr) & act)[0]:
-                slots += [h[kk], t[kk], nh[kk], nt[kk]]
-            if relpair and rr < ent.shape[0]:
-                slots.append(rr)
-            seen, uniq = set(), []
-            for e in slots:
-                if e not in seen:
-                    seen.add(e)
-                    uniq.append(e)
-            Wm = W0[rr]
-            K0 = Wm.T @ Wm
-            Wc = Wm.copy()
-            for c0 in range(0, len(uniq), C):
-                A = E1[uniq[c0:c0 + C]]
-                P = A @ Wc                     # rows p_k = Wc^T a_k
-                Q0 = (P * P).sum(1)
-                dWc = np.zeros_like(Wc)
-                for k in np.nonzero(Q0 > 1.0)[0]:
-                    p, a0 = P[k], A[k]
-                    s0 = a0 @ a0
-                    v = K0 @ p + s0 * p
-                    d, ee = p @ v, v @ v
-                    m = 0
-                    while m < max_iter:
-                        q = Q0[k] - 4 * rate * m * d + 4 * rate * rate * m * m * ee
-                        if not q > 1.0:
-                            break
-                        m += 1
-                    G = 2.0 * m * p - 2.0 * rate * m * (m - 1) * v
-                    dWc -= rate * np.outer(a0, G)
-                    dE[uniq[c0 + k]] += -rate * (Wm @ G)
-                    if stats is not None:
-                        stats["fired"] = stats.get("fired", 0) + 1
-                Wc = Wc + dWc
-            W[rr] = Wc
-        ent += dE
-        return
-    if renorm == "gs1":  # experiment: first-order Gauss-Seidel over the relation's pairs (closed-form rounds)
-        W0 = W.copy()
-        E1 = ent.copy()
-        dE = np.zeros_like(ent)
-        for rr in ra:
-            slots = []
-            for kk in np.nonzero((r == rr) & act)[0]:
-                slots += [h[kk], t[kk], nh[kk], nt[kk]]
-            if relpair and rr < ent.shape[0]:
-                slots.append(rr)
-            Wm = W0[rr]
-            K0 = Wm.T @ Wm
-            Wc = Wm.copy()
-            seen = set()
-            for e in slots:
-                if e in seen:
-                    continue
-                seen.add(e)
-                a0 = E1[e]
-                s0 = a0 @ a0
-                p = Wc.T @ a0
-                Q0 = p @ p
-                if not Q0 > 1.0:
-                    if stats is not None:
-                        stats["pairs"] = stats.get("pairs", 0) + 1
-                    continue
-                v = K0 @ p + s0 * p
-                d, ee = p @ v, v @ v
-                m = 0
-                while m < max_iter:  # |p_m|^2 with p_m = p - 2 lr m v (first order in lr)
-                    q = Q0 - 4 * rate * m * d + 4 * rate * rate * m * m * ee
-                    if not q > 1.0:
-                        break
-                    m += 1
-                G = 2.0 * m * p - 2.0 * rate * m * (m - 1) * v
-                Wc = Wc - rate * np.outer(a0, G)
-                dE[e] += -rate * (Wm @ G)
-                if stats is not None:
-                    stats["pairs"] = stats.get("pairs", 0) + 1
-                    stats["fired"] = stats.get("fired", 0) + 1
-                    stats["rounds"] = stats.get("rounds", 0) + m
-            W[rr] = Wc
-        ent += dE
         return
     W0 = W.copy()
     E1 = ent.copy()
-    dWc = np.zeros_like(W)
-    dWl = np.zeros_like(W)   # the corrections of each relation's last update
-    dE = np.zeros_like(ent)
-    dEl = np.zeros_like(ent)
-    # the last update touching each entity: (sample, update) order key
-    last_key = {}
-    for kk in np.nonzero(act)[0]:
-        for u, (hh, tt) in enumerate(((h[kk], t[kk]), (nh[kk], nt[kk]))):
-            for e in (hh, tt):
-                last_key[e] = (kk, u)
-    for rr in ra:
-        slots = []
-        ks = np.nonzero(r == rr)[0]
-        last_act = ks[act[ks]][-1]
-        for kk in ks:
+    if cons.startswith("chunk"):
+        C = int(cons[5:])
+        eps = 2.0 * rate
+        # the last active update touching every entity (its unit norm in the
+        # reference comes after every transRNorm shrink of earlier updates)
+        last_upd = {}
+        for kk in np.nonzero(act)[0]:
             for u, (hh, tt) in enumerate(((h[kk], t[kk]), (nh[kk], nt[kk]))):
-                slots += [(hh, kk, u), (tt, kk, u)] if act[kk] else [(-1, kk, u), (-1, kk, u)]
-        if relpair and rr < ent.shape[0]:
-            slots.append((rr, last_act, 1))
-        seen = set()
-        for (e, kk, u) in slots:
-            if e < 0 or (dedupe and e in seen):
-                continue
-            seen.add(e)
+                last_upd[int(hh)] = (int(kk), u)
+                last_upd[int(tt)] = (int(kk), u)
+        dE_pre = np.zeros_like(ent)
+        dE_post = np.zeros_like(ent)
+        for rr in ra:
+            items = _relation_items(r, rr, act, h, t, nh, nt, relpair, ne)
+            kl = int(np.nonzero((r == rr) & act)[0][-1])
+            head = [it for it in items if it[1] != (kl, 1) and it[1] is not None]
+            tail = [it for it in items if it[1] == (kl, 1) or it[1] is None]
+            Wc = W0[rr].copy()
+            K0 = Wc.T @ Wc
+            changed = False
+            chunks = [head[c0:c0 + C] for c0 in range(0, len(head), C)] + ([tail] if tail else [])
+            for ci, chunk in enumerate(chunks):
+                if tail and ci == len(chunks) - 1 and changed:
+                    # the relation's last update renormalises the rows (transr/trainer.cpp:178-180):
+                    # only its own shrinks outlive the batch
+                    Wc = Wc / np.sqrt((Wc ** 2).sum(1, keepdims=True))
+                A = E1[[e for e, _ in chunk]]
+                P = A @ Wc                      # rows p_k = W_c^T a_k
+                Q0 = (P * P).sum(1)
+                dW = np.zeros_like(Wc)
+                for k in np.nonzero(Q0 > 1.0)[0]:
+                    e, key = chunk[k]
+                    G, m = transr_norm_rounds(P[k], A[k], K0, Q0[k], eps, max_iter)
+                    post = (e not in last_upd) if key is None else last_upd.get(e) == key
+                    (dE_post if post else dE_pre)[e] += -rate * (Wc @ G)
+                    dW -= rate * np.outer(A[k], G)
+                    changed = True
+                    if stats is not None:
+                        stats["fired"] = stats.get("fired", 0) + 1
+                        stats["rounds"] = stats.get("rounds", 0) + m
+                if stats is not None:
+                    stats["pairs"] = stats.get("pairs", 0) + len(chunk)
+                Wc = Wc + dW
+            W[rr] = Wc
+        pre = np.nonzero(np.any(dE_pre != 0, axis=1))[0]
+        ent[pre] += dE_pre[pre]
+        ent[pre] /= np.sqrt((ent[pre] ** 2).sum(1, keepdims=True))
+        ent += dE_post
+        return
+    assert cons == "jacobi", cons
+    dWc = np.zeros_like(W)
+    for rr in ra:
+        for e in _relation_pairs(r, rr, act, h, t, nh, nt, relpair, ne):
             a0 = E1[e]
             Wm = W0[rr]
             G = np.zeros_like(a0)
@@ -318,23 +319,9 @@ def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, 
             if stats is not None:
                 stats["pairs"] = stats.get("pairs", 0) + 1
                 stats["fired"] = stats.get("fired", 0) + (it > 0)
-            if not it:
-                continue
-            # "last": a correction made before the row's last update in the batch is
-            # followed, in the reference, by that update's unit norm; the last
-            # update's own corrections persist
-            rel_post = renorm == "none" or (renorm == "last" and (kk, u) >= (last_act, 1))
-            ent_post = renorm == "none" or e not in last_key or (renorm == "last" and (kk, u) >= last_key[e])
-            (dEl if ent_post else dE)[e] += -rate * (Wm @ G)
-            (dWl if rel_post else dWc)[rr] += np.outer(-rate * a0, G)
+            ent[e] += -rate * (Wm @ G)
+            dWc[rr] += np.outer(-rate * a0, G)
     W[ra] += dWc[ra]
-    if renorm != "none":
-        W[ra] /= np.sqrt((W[ra] ** 2).sum(2, keepdims=True))
-    W[ra] += dWl[ra]
-    ec = np.nonzero(np.any(dE != 0, axis=1))[0]
-    ent[ec] += dE[ec]
-    ent[ec] /= np.sqrt((ent[ec] ** 2).sum(1, keepdims=True))
-    ent += dEl
 
 
 def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, rate, margin=1.0):

@@ -7,6 +7,8 @@ CPU model follows the same arithmetic (L1 deltas as integer sign counts), so
 the bar is the ulp-level difference of the 64-lane sums in the norms:
 1e-11 absolute per epoch, identical active counts, loss to 1e-9 relative.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -80,11 +82,22 @@ def test_transe_parallel_deterministic():
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
 
 
+def _cons_form(dim, mfma):
+    """The transRNorm form the engine runs (engine_transr_parallel.inc): the
+    per-relation chunk kernel on the matrix-core path for n <= 64, unless
+    KB2E_RPAR_CONS picks the Jacobi tile / wave kernels."""
+    ck = os.environ.get("KB2E_RPAR_CONS", "")
+    if mfma and dim <= 64 and ck not in ("tile", "jacobi"):
+        return "chunk" + os.environ.get("KB2E_RPAR_SEQ_CHUNK", "32")
+    return "jacobi"
+
+
 def _transr_vs_model(ds, dim, epochs, monkeypatch, *, St=8, compat=False, distance=0, batches=10, rate=0.01,
                      seed=3, atol=1e-9, mfma=True):
     from oracle.parallel import transr_parallel_batches
     monkeypatch.setenv("KB2E_RPAR_ST", str(St))
     monkeypatch.setenv("KB2E_RPAR_MFMA", "1" if mfma else "0")
+    cons = _cons_form(dim, mfma)
     m = orc.Model("R", dim, ds.num_entities, ds.num_relations, rate=rate, distance=distance, batches=batches,
                   transr_compat=compat)
     m.set_triples(ds.train)
@@ -103,7 +116,7 @@ def _transr_vs_model(ds, dim, epochs, monkeypatch, *, St=8, compat=False, distan
     for ep in range(epochs):
         si, sj, side = m.sample_stream(B * batches)
         lo, ao = transr_parallel_batches(pe, pr, pw, ds.train, si, sj, side, B, batches, rate=rate,
-                                         l1=distance == 0, compat=compat, work=work, St=St)
+                                         l1=distance == 0, compat=compat, work=work, St=St, cons=cons)
         lg, ag = eng.train_epoch()
         assert ag == ao, (ep, ag, ao)
         assert abs(lg - lo) <= 1e-9 * max(1.0, abs(lo))
@@ -128,6 +141,24 @@ def test_transr_parallel_cons_tile_kernel(dim, distance, St, compat, monkeypatch
     replaces by the register-resident one (kernels_transr_cons.hpp) by default."""
     monkeypatch.setenv("KB2E_RPAR_CONS", "tile")
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, distance=distance, compat=compat)
+
+
+@pytest.mark.parametrize("chunk", ["16", "64"])
+@pytest.mark.parametrize("dim,St,compat", [(20, 8, False), (50, 4, True)])
+def test_transr_parallel_chunk_sizes(dim, St, compat, chunk, monkeypatch):
+    """The per-relation transRNorm kernel with chunks of 16 and 64 pairs (32 is
+    the default): relations of the tiny set hold ~90 pairs a batch, so several
+    chunks, each seeing the matrix the earlier ones left."""
+    monkeypatch.setenv("KB2E_RPAR_SEQ_CHUNK", chunk)
+    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=compat)
+
+
+@pytest.mark.parametrize("dim,St", [(20, 8), (50, 8)])
+def test_transr_parallel_jacobi_wave_kernel(dim, St, monkeypatch):
+    """KB2E_RPAR_CONS=jacobi: the register-resident tile kernel (every pair of
+    the batch against the same matrix, corrections summed)."""
+    monkeypatch.setenv("KB2E_RPAR_CONS", "jacobi")
+    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=True)
 
 
 @pytest.mark.parametrize("mfma", [True, False])

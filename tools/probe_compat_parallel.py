@@ -4,12 +4,12 @@ from the reference's (ORDERED) trajectory?
 
 Trains the FB15k-shaped synthetic set with the reference restatement
 (oracle/orc.c = ORDERED, the reference bit for bit) and with the CPU model of
-the PARALLEL schedule (oracle/parallel.py) in its `renorm` variants, from the
+the PARALLEL schedule (oracle/parallel.py) in its transRNorm variants (`cons`: jacobi, chunk<C>, seq), from the
 same TransE-init tables and the same glibc sample stream, and prints per-epoch
 losses plus table statistics (mean matrix-row length, mean |W_r^T e|).  Test
 infrastructure only (it runs the oracle).
 
-  python tools/probe_compat_parallel.py --epochs 4 --variants none,last
+  python tools/probe_compat_parallel.py --epochs 4 --variants jacobi,chunk32
 """
 import argparse
 import json
@@ -40,7 +40,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--epochs", type=int, default=4)
     ap.add_argument("--seed-epochs", type=int, default=20)
-    ap.add_argument("--variants", default="none,all,last")
+    ap.add_argument("--variants", default="jacobi,chunk32,seq")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--shape", default="fb15k")
     args = ap.parse_args()
@@ -90,7 +90,7 @@ def main():
             sl = slice(ep * S, (ep + 1) * S)
             st = {}
             loss, act = transr_parallel_batches(pe, pr, pw, ds.train, stream[0][sl], stream[1][sl], stream[2][sl], B,
-                                                NB, rate=0.001, compat=True, work=work, renorm=v, stats=st)
+                                                NB, rate=0.001, compat=True, work=work, cons=v, stats=st)
             pl.append({"loss": loss, "active": act, **st, **table_stats(pe, pr, pw, ds.train, rng)})
             print(f"parallel[{v}] epoch {ep}: {pl[-1]} ({time.time() - t0:.0f} s)", file=sys.stderr)
         out[f"parallel_{v}"] = pl
