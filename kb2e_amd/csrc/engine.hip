@@ -159,8 +159,7 @@ struct kb2e_ctx {
     bool rpar_mfma = false;  // matrix-core tile kernels (kernels_transr_mfma.hpp)
     bool rpar_cons_wave = false;  // transRNorm rounds in one wave's registers (kernels_transr_cons.hpp)
     size_t rpar_cons_lds = 0;
-    bool rpar_cons_seq = false;   // transRNorm per relation in chunks (kernels_transr_seq.hpp)
-    int32_t rpar_seq_chunk = 32;
+    bool rpar_cons_seq = false;   // transRNorm per relation, a chain of chunks (kernels_transr_seq.hpp)
     size_t rpar_seq_lds = 0;
     DevBuf rpar_pflag, rpar_cons_tile, rpar_cpairs, rpar_cnrows;
     DevBuf rpar_y, rpar_wpart, rpar_rpart, rpar_tile_act, rpar_pair, rpar_relpair, rpar_relpair_stamp, rpar_tiles,
@@ -1655,11 +1654,17 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
             fprintf(stderr, "rpar_cons cycles: setup %llu, P0+rounds %llu, records %llu, longest block %llu, blocks %llu\n",
                     st[3], st[4], st[5], st[6], st[7]);
             if (c->rpar_cons_seq) {
-                unsigned long long q[8];
+                unsigned long long q[64];
                 cons_seq_take_stats(q);
                 fprintf(stderr, "rpar_cons chunk kernel: relations %llu, chunks %llu (most in a relation %llu), "
-                        "violators %llu, rounds %llu, cycles mean %.0f max %llu\n", q[0], q[1], q[6], q[2], q[3],
-                        q[0] ? (double)q[4] / (double)q[0] : 0.0, q[5]);
+                        "violators %llu, rounds %llu (most %llu), cycles mean %.0f max %llu\n", q[0], q[1], q[6], q[2],
+                        q[3], q[7], q[0] ? (double)q[4] / (double)q[0] : 0.0, q[5]);
+                fprintf(stderr, "rpar_cons chunk phases (prologue, issue+renorm, P+Gram+B1, K0, violators, B2, "
+                        "W update+rows+B3; violator: V, sums, rounds, record, update):");
+                for (int k = 8; k < 20; ++k) fprintf(stderr, " %llu", q[k]);
+                fprintf(stderr, "; hot relations (%llu, %llu chunks, %llu violators):", q[41], q[40], q[42]);
+                for (int k = 24; k < 36; ++k) fprintf(stderr, " %llu", q[k]);
+                fprintf(stderr, "\n");
             }
             if (c->rpar_cons_wave)
                 fprintf(stderr, "rpar_cons wave kernel: longest setup %llu, P0+rounds %llu, records %llu, a wave's "

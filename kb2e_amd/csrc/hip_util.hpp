@@ -32,6 +32,8 @@ struct DevBuf {
         free();
         if (b == 0) b = 16;
         HIPCHK(hipMalloc(&p, b));
+        // zeroed: no kernel result may depend on what an earlier engine left in the heap
+        HIPCHK(hipMemset(p, 0, b));
         bytes = b;
     }
     void free() {

@@ -1,100 +1,176 @@
 // kernels_transr_seq.hpp -- transRNorm of the PARALLEL TransR schedule per
-// relation, in chunks of the relation's pairs: Jacobi inside a chunk,
-// Gauss-Seidel across chunks (transr/trainer.cpp:35-64, :185-187; CPU model:
-// oracle/parallel.py transr_constraint, renorm="jc<C>").
+// relation, the relation's pairs one after another, each against the matrix the
+// earlier ones left (transr/trainer.cpp:35-64, :185-187; CPU model:
+// oracle/parallel.py transr_constraint, cons="chunk1").
 //
-// Why per relation.  The reference calls transRNorm(h', W'_r), transRNorm(t',
-// W'_r) and transRNorm(entity'[r], W'_r) after every update of relation r, one
-// after another, each on the matrix the previous calls left: a later pair only
+// Why per relation, in order.  The reference calls transRNorm(h', W'_r),
+// transRNorm(t', W'_r) and transRNorm(entity'[r], W'_r) after every update of
+// relation r, each on the matrix the previous calls left: a later pair only
 // shrinks W'_r if it still violates |W^T a|^2 <= 1 after the earlier pairs'
 // shrinks.  Computing every pair of the batch against the same W'_r and summing
 // the corrections (the tile kernels' Jacobi form) over-shrinks W'_r along the
 // directions the relation's entities share: on FB15k-shaped data the compat
-// loss ends 20% below the reference's and outside its seed envelope
-// (profiles/seed_envelope_r17_fb15k_R_compat.jsonl, tools/probe_compat_parallel.py).
-// Walking the relation's pairs in order, C at a time, with W_r updated after
-// every chunk keeps the coupling the reference has (loss within ~1% of the
-// reference after each epoch in the CPU model, against -5% for the sum).
+// loss ends 20% below the reference's, outside its seed envelope
+// (profiles/seed_envelope_r17_fb15k_R_compat.jsonl); in order it is inside
+// (profiles/seed_envelope_r18_*).
 //
-// Per chunk of <= C pairs (the (h', r), (t', r) pairs of the active updates in
-// (sample, update, role) order and (entity'[r], r) once, first occurrences per
-// relation per batch -- the gradient kernel's compacted lists bf.cpairs):
-//   P = A W_c                      (A: the pairs' entity rows after the unit norms)
-//   violators: |p|^2 > 1
-//   V = P_v K0 + |a|^2 P_v         (K0 = W^T W of the relation's matrix, made once)
-//   m = first round with |p - 2 lr m v|^2 <= 1   (the loop p <- p - 2 lr (K0 + |a|^2) p
-//                                                 to first order in lr)
-//   G = 2 m p - 2 lr m (m - 1) v   (sum of 2 p over the m rounds)
-//   da = -lr W_c G  -> pair records (pass 2 adds them to the entity rows)
-//   W_c <- W_c - lr A_v^T G        (the chunk's matrix corrections)
-// and the relation's matrix is written back once, so the transRNorm pass needs
-// no matrix partials.  All four products are matrix-core GEMMs
-// (v_mfma_f64_16x16x4_f64 / f32) over LDS images.
+// The pairs (the (h', r), (t', r) pairs of the active updates in (sample,
+// update, role) order, first occurrences per relation per batch -- the gradient
+// kernel's compacted lists bf.cpairs -- then (entity'[r], r)), per violator v
+// (|p_v|^2 > 1, p_v = a_v W_c, a_v the entity row after its unit norm):
+//   V = p_v K0                     (K0 = W'^T W', made at the relation's first violator)
+//   the rounds of transRNorm's loop along p and w (transr_norm_rounds): with
+//   v = V + |a|^2 p = kappa p + w, rho = 1 - 2 lr kappa,
+//   m = the first round t with rho^2t |p|^2 + (2 lr t)^2 rho^(2t-2) |w|^2 <= 1,
+//   g = 2 (S0 + 2 lr S1 kappa) p - 4 lr S1 v   (S0 = sum rho^t, S1 = sum t rho^(t-1))
+//   W_c <- W_c - lr a_v^T g
+// The pairs of the relation's last update and (entity'[r], r) come last, after
+// W_c's rows are renormalised (the reference renormalises W' at every update, so
+// only the last update's shrinks outlive the batch); the entity pass
+// renormalises a row between the deltas of its earlier pairs and those of its
+// own last update (bf.last_renorm, kernels_transr_parallel.hpp).
+//
+// The work is cut so that only the violators are sequential.  Per chunk of 32
+// pairs, all four waves make P = A W_c and the Gram matrix A A^T on the matrix
+// cores (16 x 16 tiles); then one wave walks the chunk's pairs: the first pair
+// with |p_j|^2 > 1 is the next violator v, its V row, scalars, rounds and g are
+// made with lane c holding column c, and its shrink reaches every later pair of
+// the chunk as P_j -= lr (a_j . a_v) g (the Gram entry), |p_j|^2 made afresh --
+// no barrier between violators.  The chunk's violators then update W_c (the G
+// rows kept in P), before the next chunk's P.  ~1.7 of 16 pairs violate on
+// FB15k-shaped data.  The pair records da = -lr W G are made afterwards, one
+// wave a violator, over the final matrix (transr_cons_da_kernel: first order
+// the same, off the chain).
 #pragma once
 
 #include "kernels_transr_mfma.hpp"
 
 namespace kb2e {
 
-constexpr int kSeqThreads = 256;
-constexpr int kSeqMaxTiles = 256;  // tiles of one relation handled per window of the prefix table
+constexpr int kChainRows = 32;      // pairs a chunk: two MFMA row tiles of projections and Gram rows
+constexpr int kChainThreads = 256;  // four waves; wave w < NB owns column slice w
+constexpr int kSeqMaxTiles = 256;   // tiles of one relation a window (the prefix table)
+constexpr int kChainList = 2048;    // pairs of one relation a window (entity and slot lists in LDS)
 
-// LDS row stride of the images: n rounded up to even (16-byte rows of FP64 pairs)
-__host__ __device__ constexpr int seq_ld(int n) { return (n + 1) & ~1; }
-
-// LDS bytes: Wc [n][L] | K0 [n][L] | A [C][L] | P [C][L] | V [C][L] | |p|^2 [C] | ints
+// LDS (elements of T): W_c [NP][L] | K0 [NP][L] | A [2][R][L] | P [R][L] |
+// Gram [R][R + 1] | |p|^2 partials [4][R] | row partials [4][NP] ; ints: pair
+// entities, slots [2][kChainList] | pre [kSeqMaxTiles + 1] | misc [8]
 template <typename T>
-__host__ __device__ constexpr size_t seq_lds(int n, int C) {
-    return sizeof(T) * ((size_t)seq_ld(n) * (2 * (size_t)n + 3 * (size_t)C) + (size_t)C) +
-           sizeof(int) * (size_t)(5 * C + kSeqMaxTiles + 1 + 8);
+__host__ __device__ constexpr size_t chain_lds(int n) {
+    return sizeof(T) * ((size_t)rm_np(n) * rm_ld(n) * 2 + 3 * (size_t)kChainRows * rm_ld(n) +
+                        (size_t)kChainRows * (kChainRows + 1) + 4 * kChainRows + 4 * (size_t)rm_np(n)) +
+           sizeof(int) * (size_t)(2 * kChainList + kSeqMaxTiles + 1 + 8);
 }
 
-// KB2E_RPAR_STATS: relations, chunks, violators, rounds, cycles (sum, max) of the blocks
-static __device__ unsigned long long g_seq_stats[8];
+// KB2E_RPAR_STATS: 0 relations, 1 chunks, 2 violators, 3 rounds, 4 cycles sum, 5 max, 6 most chunks, 7 most rounds,
+// 8..23 cycles of the phases (thread 0: prologue, load issue, S1 MFMA issue, S1 sums, B1, mask + K0, S3 MFMA
+// issue, S3 sums, rows + B2, rounds, shuffles, S5, S6), 24..39 the same over relations of >= 40 chunks,
+// 40 their chunks, 41 their count
+static __device__ unsigned long long g_seq_stats[64];
 
-template <typename T, int NP, int C>
-__global__ __launch_bounds__(kSeqThreads) void transr_cons_seq_kernel(RParArgs a, RParBufs<T> bf) {
-    static_assert(C % 16 == 0 && C <= 64, "chunk: multiple of 16, one wave of lanes");
-    constexpr int kPre = (C * NP + kSeqThreads - 1) / kSeqThreads;  // prefetched row elements a thread
+// sums over the 16 lanes of a DPP row (lanes l & ~15 ... l | 15), in every lane of
+// the row, of K values at once (independent chains, interleaved): the first four
+// steps of wave_sum (kernels_common.hpp)
+template <typename T, int K>
+__device__ __forceinline__ void row16_sums(T (&v)[K]) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] += dpp_ror<8>(v[k]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] += dpp_ror<4>(v[k]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] += dpp_ror<2>(v[k]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] += dpp_ror<1>(v[k]);
+}
+
+// wave-wide sums of K values at once (interleaved DPP chains, kernels_common.hpp
+// wave_sum), the totals in every lane
+template <typename T, int K>
+__device__ __forceinline__ void wave_sums(T (&v)[K]) {
+    row16_sums<T, K>(v);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] += dpp_mov<kDppBcast15>(v[k]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] += dpp_mov<kDppBcast31>(v[k]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = readlane_f(v[k], 63);
+}
+
+// The rounds m of transRNorm's loop and the sums S0 = sum_{t<m} rho^t,
+// S1 = sum_{t<m} t rho^(t-1) (oracle/parallel.py transr_norm_rounds): m is the
+// first t with rho^2t Q0 + eps^2 t^2 rho^(2t-2) w2 <= 1.  A handful of FMAs a
+// round (m is 1-3 for almost every violator), cheaper than the closed form's pow.
+template <typename T>
+__device__ __forceinline__ int transr_rounds(T Q0, T w2, T eps, T rho, T& S0, T& S1) {
+    const T e2w = eps * eps * w2;
+    T rt = T(1), rtm1 = T(0);  // rho^t, rho^(t-1) (0 at t = 0)
+    S0 = T(0);
+    S1 = T(0);
+    int m = 0;
+    while (m < kRParMaxIter && rt * rt * Q0 + e2w * (T)m * (T)m * rtm1 * rtm1 > T(1)) {
+        S0 += rt;
+        S1 += (T)m * rtm1;
+        rtm1 = rt;
+        rt *= rho;
+        ++m;
+    }
+    return m;
+}
+
+// KS = ceil(n / 4): the live k-steps of a contraction over n, a compile-time
+// count so that the MFMA chains are straight-line code (no per-step branches)
+template <typename T, int KS>
+__global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParArgs a, RParBufs<T> bf) {
+    using M = Mfma16<T>;
+    static_assert(sizeof(T) == 8, "the D-row / k-step identity below is the FP64 fragment layout");
+    constexpr int NB = (4 * KS + 15) / 16;  // column slices of 16
+    constexpr int NP = 16 * NB, L = NP + 2, R = kChainRows, LG = R + 1;
     const int t0 = a.batch_t0[a.batch], t1 = a.batch_t0[a.batch + 1];
     const int g0 = blockIdx.x;  // tile index within the batch
     if (t0 + g0 >= t1) return;
     const int r = a.td_r[t0 + g0];
     if (g0 > 0 && a.td_r[t0 + g0 - 1] == r) return;  // not the relation's first tile
-    const int n = a.n, ld = a.ld, L = seq_ld(n);
-    const int w = threadIdx.x >> 6, l = lane_id();
+    const int n = a.n, ld = a.ld;
+    const int w = threadIdx.x >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
+    const bool mine = w < NB;  // this wave owns a column slice (K0, the W_c update)
+    const int col = 16 * w + l16;
     const T lr = (T)a.lr;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* Wc = (T*)smem;
-    T* K0 = Wc + n * L;
-    T* A = K0 + n * L;
-    T* P = A + C * L;
-    T* V = P + C * L;
-    T* qv = V + C * L;                // [C] |p|^2 of the chunk's pairs
-    int* ents = (int*)(qv + C);       // [C] this chunk's pairs: entity, slot (-2: (entity[r], r))
-    int* slots = ents + C;
-    int* nents = slots + C;           // [C] the next chunk's
-    int* nslots = nents + C;
-    int* vio = nslots + C;            // [C] this chunk's violators (chunk positions)
-    int* pre = vio + C;               // [kSeqMaxTiles + 1] exclusive prefix of the window's tile pair counts
-    int* misc = pre + kSeqMaxTiles + 1;  // 1 violators, 2 K0 made, 3 relation pair, 4 last sample, 5 tiles, 6 tail
+    T* K0 = Wc + NP * L;
+    T* Abuf = K0 + NP * L;      // [2][R][L] the chunk's entity rows (double buffered)
+    T* P = Abuf + 2 * R * L;    // [R][L] projections, then G rows of the violators
+    T* Gm = P + R * L;          // [R][LG] Gram matrix A A^T of the chunk
+    T* qpart = Gm + R * LG;     // [NB][R] |p|^2 partials of the column slices
+    T* rp = qpart + 4 * R;      // [4][NP] row partials of the tail renorm
+    int* pe = (int*)(rp + 4 * NP);  // the window's pairs: entities [kChainList], slots [kChainList]
+    int* ps = pe + kChainList;
+    int* pre = ps + kChainList;
+    int* misc = pre + kSeqMaxTiles + 1;
     const long long ck0 = clock64();
-    unsigned long long n_chunks = 0, n_vio = 0, n_rounds = 0;
+    unsigned long long n_chunks = 0, n_vio = 0, n_rounds = 0, max_m = 0;
+    unsigned long long ph[16] = {};  // stats: cycles of the phases (thread 0; see g_seq_stats)
+    long long tq = ck0;
+    auto tick = [&](int k) {
+        if (bf.stats && threadIdx.x == 0) {
+            const long long t = clock64();
+            ph[k] += (unsigned long long)(t - tq);
+            tq = t;
+        }
+    };
 
-    // the relation's matrix W'_r (after the gradient step's unit row norms)
-    for (int idx = threadIdx.x; idx < n * n; idx += kSeqThreads) {
-        const int j = idx / n, i = idx % n;
-        Wc[j * L + i] = bf.W[((int64_t)r * n + j) * ld + i];
+    // W'_r, zero padded to NP x NP
+    for (int idx = threadIdx.x; idx < NP * NP; idx += kChainThreads) {
+        const int j = idx / NP, i = idx % NP;
+        Wc[j * L + i] = (j < n && i < n) ? bf.W[((int64_t)r * n + j) * ld + i] : T(0);
     }
-    if (threadIdx.x == 0) misc[2] = 0;
-
     // The relation's pairs in order: its tiles' compacted lists, except that the
     // (entity'[r], r) pair, which the gradient kernel appends to the relation's
-    // first tile, goes last (as the reference's last call of the batch; the
-    // order, and so the result, does not depend on the tile size).  Windows of
-    // up to kSeqMaxTiles tiles hold the prefix table.
+    // first tile, goes last (the order, and so the result, does not depend on the
+    // tile size); the relation's last active sample kl, its tile, and how many
+    // of the pairs belong to kl's corrupted-triple update (the tail).
     if (w == 0) {
-        int run = 0;  // the relation's tiles: a run of equal td_r from g0
+        int run = 0;
         for (int m0 = 0;; m0 += kWave) {
             const int g = g0 + m0 + l;
             const uint64_t b = __ballot(t0 + g < t1 && a.td_r[t0 + g] == r);
@@ -104,8 +180,6 @@ __global__ __launch_bounds__(kSeqThreads) void transr_cons_seq_kernel(RParArgs a
         }
         const int c0 = bf.cnrows[g0] & 127;
         const int rel = c0 > 0 && bf.cpairs[(int64_t)g0 * 2 * kCPairs + kCPairs + c0 - 1] == -2;
-        // the relation's last active sample kl (its last update: the corrupted triple,
-        // kl 2 + 1) and how many of the pairs (first occurrences) belong to that update
         int kl = -1, gt = -1;
         for (int g = g0 + run - 1; g >= g0 && kl < 0; --g) {
             const int cs = a.td_cnt[t0 + g] & 255;
@@ -131,42 +205,45 @@ __global__ __launch_bounds__(kSeqThreads) void transr_cons_seq_kernel(RParArgs a
     }
     __syncthreads();
     const int run = misc[5], has_rel = misc[3], g_tail = misc[4], n_tail = misc[6];
-    for (int gw = g0; gw < g0 + run || gw == g0; gw += kSeqMaxTiles) {
-        const int ntile = g0 + run - gw < kSeqMaxTiles ? g0 + run - gw : kSeqMaxTiles;
-        const bool last = gw + ntile == g0 + run;
+    bool have_k0 = false, changed = false;
+    tick(0);
+    int chunk_no = 0;  // chunks so far (row buffer parity)
+    // windows of at most kSeqMaxTiles tiles and kChainList - 1 pairs (FB15k's hottest
+    // relation holds ~1000 pairs a batch: one window)
+    for (int gw = g0; gw < g0 + run || gw == g0;) {
         if (w == 0) {  // exclusive prefix of the window's tile pair counts (the relation pair left out)
-            int carry = 0;
-            for (int m0 = 0; m0 < ntile; m0 += kWave) {
+            const int nt = g0 + run - gw < kSeqMaxTiles ? g0 + run - gw : kSeqMaxTiles;
+            int carry = 0, fit = 0;
+            for (int m0 = 0; m0 < nt; m0 += kWave) {
                 const int g = m0 + l;
-                int c = g < ntile ? (bf.cnrows[gw + g] & 127) : 0;
+                int c = g < nt ? (bf.cnrows[gw + g] & 127) : 0;
                 if (gw + g == g0 && has_rel) c -= 1;
-                int x = c;  // inclusive wave scan
+                int x = c;
 #pragma unroll
                 for (int s = 1; s < kWave; s <<= 1) {
                     const int y = __shfl_up(x, s);
                     if (l >= s) x += y;
                 }
-                if (g < ntile) pre[g] = carry + x - c;
+                if (g < nt) pre[g] = carry + x - c;
+                // tiles whose pairs (and the relation pair) still fit the list
+                fit += __builtin_popcountll(__ballot(g < nt && carry + x <= kChainList - 1));
                 carry += __shfl(x, kWave - 1);
             }
-            if (l == 0) pre[ntile] = carry;
+            if (l == 0) {
+                if (fit == nt) pre[nt] = carry;
+                misc[0] = fit;
+            }
         }
         __syncthreads();
-        const int ntp = pre[ntile];                       // pairs from the window's tiles
+        const int ntile = misc[0];
+        const bool last = gw + ntile == g0 + run;
+        const int ntp = pre[ntile];
         const int npairs = ntp + (last && has_rel ? 1 : 0);
-        // the last update's pairs and (entity'[r], r) form the final chunk (in the last window)
         const int tail_start = last && g_tail >= gw ? ntp - n_tail : npairs;
-        auto chunk_end = [&](int b) { return b < tail_start ? (b + C < tail_start ? b + C : tail_start) : npairs; };
-        // pair `base + l` (wave 0, lane l < C): the tile holding that flat index
-        // (binary search in pre), its entity and slot into registers
-        auto fetch_ids = [&](int base, int& e, int& s) {
-            e = -1;
-            s = -3;
-            const int f = base + l;
-            if (w == 0 && l < C && f == ntp && f < npairs) {
-                e = r;
-                s = -2;
-            } else if (w == 0 && l < C && f < ntp) {
+        // the window's pairs into LDS, every thread a pair at a time
+        for (int f = threadIdx.x; f < npairs; f += kChainThreads) {
+            int e = r, sl = -2;
+            if (f < ntp) {
                 int lo = 0, hi = ntile - 1;
                 while (lo < hi) {
                     const int mid = (lo + hi + 1) >> 1;
@@ -175,194 +252,325 @@ __global__ __launch_bounds__(kSeqThreads) void transr_cons_seq_kernel(RParArgs a
                 }
                 const int32_t* cp = bf.cpairs + (int64_t)(gw + lo) * 2 * kCPairs;
                 e = cp[f - pre[lo]];
-                s = cp[kCPairs + f - pre[lo]];
+                sl = cp[kCPairs + f - pre[lo]];
             }
-        };
-        // the chunk's entity rows into registers (issued early, stored after the chunk)
-        T pre_rows[kPre];
-        auto load_rows = [&](const int* e_in) {
-#pragma unroll
-            for (int q = 0; q < kPre; ++q) {
-                const int idx = threadIdx.x + q * kSeqThreads;
-                const int k = idx / NP, j = idx % NP;
-                const int e = (k < C) ? e_in[k] : -1;
-                pre_rows[q] = (e >= 0 && j < n) ? bf.ent[(int64_t)e * ld + j] : T(0);
-            }
-        };
-        auto store_rows = [&]() {
-#pragma unroll
-            for (int q = 0; q < kPre; ++q) {
-                const int idx = threadIdx.x + q * kSeqThreads;
-                const int k = idx / NP, j = idx % NP;
-                if (k < C && j < L) A[k * L + j] = j < n ? pre_rows[q] : T(0);
-            }
-        };
-        {
-            int e, s;
-            fetch_ids(0, e, s);
-            if (w == 0 && l < C) {
-                ents[l] = e;
-                slots[l] = s;
-            }
+            pe[f] = e;
+            ps[f] = sl;
         }
+        // chunks of R pairs; the relation's last update's pairs (and (entity'[r], r)) alone
+        auto chunk_end = [&](int b) {
+            return b < tail_start ? (b + R < tail_start ? b + R : tail_start) : npairs;
+        };
+        // rows of the chunk [b, e): R x NP elements, R NP / 256 a thread, into registers.
+        // Every load is issued (a valid address when the element is padding) and the
+        // padding zeroed when stored, so no register is written under a branch while a
+        // load into it may be in flight.
+        constexpr int kRowsPer = R * NP / kChainThreads;
+        T rows[kRowsPer];
+        uint32_t rows_ok = 0;
+        auto load_rows = [&](int b, int e) {
+            int ent[kRowsPer];
+#pragma unroll
+            for (int q = 0; q < kRowsPer; ++q) {
+                const int f = b + (threadIdx.x + q * kChainThreads) / NP;
+                ent[q] = pe[f < kChainList ? f : kChainList - 1];
+            }
+            rows_ok = 0;
+#pragma unroll
+            for (int q = 0; q < kRowsPer; ++q) {
+                const int idx = threadIdx.x + q * kChainThreads;
+                const int k = idx / NP, j = idx % NP;
+                const bool ok = b + k < e && ent[q] >= 0 && j < n;
+                rows[q] = bf.ent[ok ? (uint32_t)ent[q] * (uint32_t)ld + (uint32_t)j : 0u];
+                rows_ok |= (ok ? 1u : 0u) << q;
+            }
+        };
+        auto store_rows = [&](int b) {
+#pragma unroll
+            for (int q = 0; q < kRowsPer; ++q) {
+                const int idx = threadIdx.x + q * kChainThreads;
+                Abuf[b * R * L + (idx / NP) * L + idx % NP] = ((rows_ok >> q) & 1) ? rows[q] : T(0);
+            }
+        };
         __syncthreads();
-        load_rows(ents);
-        store_rows();
+        load_rows(0, chunk_end(0));
+        store_rows(chunk_no & 1);
         __syncthreads();
-        for (int base = 0; base < npairs; base = chunk_end(base)) {
-            const int cc = chunk_end(base) - base;
-            ++n_chunks;
-            // the next chunk's ids (their loads overlap this chunk's projections)
+        for (int base = 0; base < npairs; ++chunk_no) {
             const int nbase = chunk_end(base);
-            const bool more = nbase < npairs;
-            int e_next = -1, s_next = -3;
-            if (more) fetch_ids(nbase, e_next, s_next);
-            if (base == tail_start && misc[2]) {
+            const int cc = nbase - base;
+            const int nrt = cc > 16 ? 2 : 1;  // row tiles of the chunk
+            const T* A = Abuf + (chunk_no & 1) * R * L;
+            ++n_chunks;
+            load_rows(nbase, nbase < npairs ? chunk_end(nbase) : nbase);  // next chunk's rows in flight
+            if (base == tail_start && changed) {
                 // the relation's last update renormalises the rows before its own pairs'
-                // shrinks (transr/trainer.cpp:178-180): a wave a row
-                for (int j = w; j < n; j += kSeqThreads / kWave) {
-                    const T x = l < n ? Wc[j * L + l] : T(0);
-                    const T len = sqrt(wave_sum(x * x));
-                    if (l < n) Wc[j * L + l] = x / len;
+                // shrinks (transr/trainer.cpp:178-180): row sums over the slices, then each
+                // wave scales its own columns
+                if (mine && l < NP) {
+                    T sq = T(0);
+                    if (l < n)
+                        for (int i = 0; i < 16; ++i) sq += Wc[l * L + 16 * w + i] * Wc[l * L + 16 * w + i];
+                    rp[w * NP + l] = sq;
+                }
+                __syncthreads();
+                if (mine && l < n) {
+                    T ss = rp[l];
+                    for (int v = 1; v < NB; ++v) ss += rp[v * NP + l];
+                    const T len = sqrt(ss);
+                    for (int i = 0; i < 16; ++i) Wc[l * L + 16 * w + i] = Wc[l * L + 16 * w + i] / len;
                 }
                 __syncthreads();
             }
-            // P = A W_c
-            block_gemm<T>(C / 16, NP / 16, rm_k4(n),
-                          [&](int ar, int k) { return (ar < cc && k < n) ? A[ar * L + k] : T(0); },
-                          [&](int k, int bc) { return (k < n && bc < n) ? Wc[k * L + bc] : T(0); },
-                          [&](int m, int c, T v) {
-                              if (m < C && c < n) P[m * L + c] = v;
-                          });
-            if (more && w == 0 && l < C) {
-                nents[l] = e_next;
-                nslots[l] = s_next;
-            }
-            __syncthreads();
-            if (more) load_rows(nents);  // the next chunk's rows in flight during this one
-            {  // |p|^2: kSeqThreads / C threads a pair
-                constexpr int TPP = kSeqThreads / C;
-                const int k = threadIdx.x / TPP, part = threadIdx.x % TPP;
-                T q = T(0);
-                if (k < cc)
-                    for (int i = part; i < n; i += TPP) q += P[k * L + i] * P[k * L + i];
+            tick(1);
+            // Phase A, all waves: P = A W_c and the Gram matrix A A^T of the chunk, 16 x 16
+            // MFMA tiles dealt round the waves; |p|^2 partials per column slice.
+            {
+                const int ntiles = nrt * NB + nrt * nrt;
+                for (int tl = w; tl < ntiles; tl += kChainThreads / kWave) {
+                    const bool gram = tl >= nrt * NB;
+                    const int rt = gram ? (tl - nrt * NB) / nrt : tl / NB;
+                    const int cb = gram ? (tl - nrt * NB) % nrt : tl % NB;
+                    typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
+                    T av[KS], bv[KS];
 #pragma unroll
-                for (int sft = 1; sft < TPP; sft <<= 1) q += __shfl_xor(q, sft);
-                if (part == 0) qv[k] = q;
-            }
-            __syncthreads();
-            // violators |p|^2 > 1 (wave 0, lane = pair)
-            if (w == 0) {
-                const bool v = l < cc && qv[l < C ? l : 0] > T(1);
-                const uint64_t m = __ballot(v);
-                if (v) vio[__builtin_popcountll(m & ((1ull << l) - 1))] = l;
-                if (l == 0) misc[1] = __builtin_popcountll(m);
-                const int s = l < cc ? slots[l] : -3;
-                if (l < cc && !v && s >= 0) bf.pflag[s] = 0;
-                if (v && s >= 0) bf.pflag[s] = 1;
-                if (v && s == -2) bf.relpair_stamp[r] = bf.stamp;
-            }
-            __syncthreads();
-            const int nv = misc[1];
-            if (nv > 0) {
-                n_vio += nv;
-                if (!misc[2]) {  // K0 = W^T W once (W_c is still W'_r before the first violator)
-                    block_gemm<T>(NP / 16, NP / 16, rm_k4(n),
-                                  [&](int ar, int k) { return (ar < n && k < n) ? Wc[k * L + ar] : T(0); },
-                                  [&](int k, int bc) { return (k < n && bc < n) ? Wc[k * L + bc] : T(0); },
-                                  [&](int m, int c, T v) {
-                                      if (m < n && c < n) K0[m * L + c] = v;
-                                  });
-                    __syncthreads();
-                    if (threadIdx.x == 0) misc[2] = 1;
-                }
-                // V = P_v K0 (rows: the compacted violators)
-                block_gemm<T>((nv + 15) / 16, NP / 16, rm_k4(n),
-                              [&](int ar, int k) { return (ar < nv && k < n) ? P[vio[ar] * L + k] : T(0); },
-                              [&](int k, int bc) { return (k < n && bc < n) ? K0[k * L + bc] : T(0); },
-                              [&](int m, int c, T v) {
-                                  if (m < nv && c < n) V[m * L + c] = v;
-                              });
-                __syncthreads();
-                // per violator (a wave each): the rounds of transRNorm's loop in closed
-                // form (oracle/parallel.py transr_norm_rounds): v = (K0 + |a|^2) p =
-                // kappa p + w, rho = 1 - eps kappa, |p_t|^2 = rho^2t Q0 + eps^2 t^2
-                // rho^(2t-2) |w|^2, G = 2 (S0 p - eps S1 w) -> V
-                const T eps = T(2) * lr;
-                for (int v = w; v < nv; v += kSeqThreads / kWave) {
-                    const int k = vio[v];
-                    const T ai = l < n ? A[k * L + l] : T(0);
-                    const T pi = l < n ? P[k * L + l] : T(0);
-                    const T s0 = wave_sum(ai * ai);
-                    const T vi = l < n ? V[v * L + l] + s0 * pi : T(0);
-                    const T q0 = wave_sum(pi * pi);
-                    const T kappa = wave_sum(pi * vi) / q0;
-                    const T wi = l < n ? vi - kappa * pi : T(0);
-                    const T w2 = wave_sum(wi * wi);
-                    const T rho = T(1) - eps * kappa;
-                    int m = 0;
-                    T S0 = T(0), S1 = T(0), rt = T(1), rtm1 = T(0);
-                    while (m < kRParMaxIter) {
-                        const T mm = (T)m;
-                        if (!(rt * rt * q0 + eps * eps * mm * mm * rtm1 * rtm1 * w2 > T(1))) break;
-                        S0 += rt;
-                        S1 += mm * rtm1;
-                        ++m;
-                        rtm1 = rt;
-                        rt *= rho;
+                    for (int s = 0; s < KS; ++s) {
+                        av[s] = A[(rt * 16 + l16) * L + 4 * s + kq];
+                        bv[s] = gram ? A[(cb * 16 + l16) * L + 4 * s + kq] : Wc[(4 * s + kq) * L + cb * 16 + l16];
                     }
-                    if (l == 0) n_rounds += (unsigned long long)m;
-                    if (l < n) V[v * L + l] = T(2) * (S0 * pi - eps * S1 * wi);
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) acc = M::mma(av[s], bv[s], acc);
+                    if (gram) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) Gm[(rt * 16 + kq + 4 * q) * LG + cb * 16 + l16] = acc[q];
+                    } else {
+                        T sp[4];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            P[(rt * 16 + kq + 4 * q) * L + cb * 16 + l16] = acc[q];
+                            sp[q] = acc[q] * acc[q];
+                        }
+                        row16_sums<T, 4>(sp);
+                        if (l16 == 0) {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) qpart[cb * R + rt * 16 + kq + 4 * q] = sp[q];
+                        }
+                    }
+                }
+            }
+            __syncthreads();  // B1
+            tick(2);
+            // |p_j|^2 of pair j on lanes j and j + 32 of every wave
+            const int j = l & (R - 1);
+            T q = T(0);
+            if (j < cc) {
+                q = qpart[j];
+                for (int v = 1; v < NB; ++v) q += qpart[v * R + j];
+            }
+            const bool anyv = __ballot(j < cc && q > T(1)) != 0;
+            if (anyv && !have_k0) {  // K0[:, slice] = W^T W[:, slice] (W_c is still W'_r here)
+                have_k0 = true;
+                if (mine) {
+#pragma unroll
+                    for (int ib = 0; ib < NB; ++ib) {
+                        typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
+                        T av[KS], bv[KS];
+#pragma unroll
+                        for (int s = 0; s < KS; ++s) {
+                            av[s] = Wc[(4 * s + kq) * L + ib * 16 + l16];
+                            bv[s] = Wc[(4 * s + kq) * L + col];
+                        }
+#pragma unroll
+                        for (int s = 0; s < KS; ++s) acc = M::mma(av[s], bv[s], acc);
+#pragma unroll
+                        for (int qq = 0; qq < 4; ++qq) K0[(ib * 16 + kq + 4 * qq) * L + col] = acc[qq];
+                    }
                 }
                 __syncthreads();
-                // da = -lr W_c G -> the pair records
-                block_gemm<T>((nv + 15) / 16, NP / 16, rm_k4(n),
-                              [&](int ar, int k) { return (ar < nv && k < n) ? V[ar * L + k] : T(0); },
-                              [&](int k, int bc) { return (k < n && bc < n) ? Wc[bc * L + k] : T(0); },
-                              [&](int m, int j, T v) {
-                                  if (m < nv && j < n) {
-                                      const int s = slots[vio[m]];
-                                      T* dst = s >= 0 ? bf.pair + (int64_t)s * ld : bf.relpair + (int64_t)r * ld;
-                                      dst[j] = -lr * v;
-                                  }
-                              });
-                __syncthreads();
-                // W_c -= lr A_v^T G
-                block_gemm<T>(NP / 16, NP / 16, rm_k4(nv),
-                              [&](int ar, int k) { return (ar < n && k < nv) ? A[vio[k] * L + ar] : T(0); },
-                              [&](int k, int bc) { return (k < nv && bc < n) ? V[k * L + bc] : T(0); },
-                              [&](int j, int i, T v) {
-                                  if (j < n && i < n) Wc[j * L + i] -= lr * v;
-                              });
-                __syncthreads();
             }
-            if (more) {  // the next chunk in place
-                store_rows();
-                if (w == 0 && l < C) {
-                    ents[l] = nents[l];
-                    slots[l] = nslots[l];
+            tick(3);
+            // Phase B, wave 0: the pairs in order, each against the matrix the earlier
+            // ones left (transr/trainer.cpp:35-64 per pair).  A violator v's shrink
+            // W_c -= lr a_v^T g_v moves every later pair's projection by
+            // -lr (a_j . a_v) g_v: applied to the P rows and |p_j|^2 at once; lane c
+            // holds column c for the violator's own quantities.
+            if (w == 0 && anyv) {
+                uint32_t vmask = 0;
+                int cursor = 0;
+                const T eps = T(2) * lr;
+                for (;;) {
+                    const uint64_t cand = __ballot(l < R && j < cc && j >= cursor && q > T(1));
+                    if (!cand) break;
+                    const int v = __builtin_ctzll(cand);
+                    const int c = l;  // column
+                    const T pv = c < NP ? P[v * L + c] : T(0);
+                    const T av = c < NP ? A[v * L + c] : T(0);
+                    // V[c] = sum_i p_v[i] K0[i][c], four chains
+                    T vv4[4] = {T(0), T(0), T(0), T(0)};
+                    const int cK = c < NP ? c : 0;
+#pragma unroll
+                    for (int t = 0; t < KS; ++t)
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            vv4[u] = fma(P[v * L + 4 * t + u], K0[(4 * t + u) * L + cK], vv4[u]);
+                    const T Vc = c < n ? (vv4[0] + vv4[1]) + (vv4[2] + vv4[3]) : T(0);
+                    tick(7);
+                    T s3[3] = {pv * Vc, Vc * Vc, av * av};
+                    wave_sums<T, 3>(s3);
+                    tick(8);
+                    const T pp = readlane_f(q, v);
+                    const T pV = s3[0], VV = s3[1], aa = s3[2];
+                    const T pvd = pV + aa * pp, vvd = VV + T(2) * aa * pV + aa * aa * pp;
+                    const T kappa = pvd / pp;
+                    const T w2t = vvd - kappa * pvd;
+                    const T w2 = w2t > T(0) ? w2t : T(0);
+                    const T rho = T(1) - eps * kappa;
+                    T S0, S1;
+                    const int m = transr_rounds(pp, w2, eps, rho, S0, S1);
+                    n_rounds += (unsigned long long)m;
+                    max_m = max_m > (unsigned long long)m ? max_m : (unsigned long long)m;
+                    const T cpf = T(2) * (S0 + eps * S1 * kappa), cvf = T(2) * eps * S1;
+                    const T g = c < n ? cpf * pv - cvf * (Vc + aa * pv) : T(0);
+                    tick(9);
+                    if (c < NP) P[v * L + c] = g;  // the violator's row now holds G
+                    {  // the pair record (da = -lr W G made later)
+                        const int sl = ps[base + v];
+                        T* dst = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
+                        if (c < n) dst[c] = g;
+                    }
+                    tick(10);
+                    // the later pairs: P[j] -= lr (a_j . a_v) g, |p_j|^2 afresh (lane j: half
+                    // l >> 5 of the columns)
+                    if (j > v && j < cc) {
+                        // blocks of 16 columns: all loads of a block, then its stores (a store
+                        // between loads would make every load wait for it)
+                        const T gl = -lr * Gm[j * LG + v];
+                        const int c0 = (l >> 5) * (NP / 2);
+                        constexpr int KB = (NP / 2) % 16 == 0 ? 16 : 8;  // divides NP / 2
+                        T s4[4] = {T(0), T(0), T(0), T(0)};
+#pragma unroll
+                        for (int b0 = 0; b0 < NP / 2; b0 += KB) {
+                            T x[KB], gg[KB];
+#pragma unroll
+                            for (int u = 0; u < KB; ++u) {
+                                x[u] = P[j * L + c0 + b0 + u];
+                                gg[u] = P[v * L + c0 + b0 + u];
+                            }
+#pragma unroll
+                            for (int u = 0; u < KB; ++u) {
+                                x[u] = fma(gl, gg[u], x[u]);
+                                s4[u & 3] = fma(x[u], x[u], s4[u & 3]);
+                            }
+#pragma unroll
+                            for (int u = 0; u < KB; ++u) P[j * L + c0 + b0 + u] = x[u];
+                        }
+                        q = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+                    }
+                    {
+                        const T other = __shfl_xor(q, 32);
+                        if (j > v && j < cc) q += other;
+                    }
+                    vmask |= 1u << v;
+                    cursor = v + 1;
+                    ++n_vio;
+                    tick(11);
                 }
-                __syncthreads();
+                if (l < cc) {  // the chunk's pair flags; (entity'[r], r) marks the relation
+                    const int sl = ps[base + l];
+                    const bool vio = (vmask >> l) & 1;
+                    if (sl >= 0) bf.pflag[sl] = vio ? 1 : 0;
+                    else if (vio) bf.relpair_stamp[r] = bf.stamp;
+                }
+                if (l == 0) misc[1] = (int)vmask;
+            } else if (w == 0 && l < cc) {
+                const int sl = ps[base + l];
+                if (sl >= 0) bf.pflag[sl] = 0;
             }
+            tick(4);
+            __syncthreads();  // B2
+            tick(5);
+            if (anyv) {
+                // W_c[:, slice] -= lr sum_v A[v]^T G[v] over the chunk's violators
+                const uint32_t vmask = (uint32_t)misc[1];
+                if (vmask) changed = true;
+                if (mine) {
+                    T wv[KS];
+#pragma unroll
+                    for (int t = 0; t < KS; ++t) wv[t] = Wc[(kq + 4 * t) * L + col];
+                    for (uint32_t mm = vmask; mm; mm &= mm - 1) {
+                        const int v = __builtin_ctz(mm);
+                        const T gl = -lr * P[v * L + col];
+#pragma unroll
+                        for (int t = 0; t < KS; ++t) wv[t] = fma(A[v * L + kq + 4 * t], gl, wv[t]);
+                    }
+#pragma unroll
+                    for (int t = 0; t < KS; ++t) Wc[(kq + 4 * t) * L + col] = wv[t];
+                }
+            }
+            store_rows((chunk_no & 1) ^ 1);  // (zeros past the window's last chunk: unread)
+            __syncthreads();  // B3: the next chunk's rows and W_c
+            tick(6);
+            base = nbase;
         }
-        __syncthreads();
+        gw += ntile;
+        if (gw >= g0 + run) break;
     }
-    // the relation's matrix back (the transRNorm pass adds no partials)
-    for (int idx = threadIdx.x; idx < n * n; idx += kSeqThreads) {
-        const int j = idx / n, i = idx % n;
-        bf.W[((int64_t)r * n + j) * ld + i] = Wc[j * L + i];
-    }
+    // the relation's matrix back: each wave its column slice (the transRNorm pass adds no partials)
+    if (mine && col < n)
+        for (int jj = 0; jj < n; ++jj) bf.W[((int64_t)r * n + jj) * ld + col] = Wc[jj * L + col];
     if (bf.stats) {
         if (threadIdx.x == 0) {
             const unsigned long long cyc = (unsigned long long)(clock64() - ck0);
             atomicAdd(&g_seq_stats[0], 1ull);
             atomicAdd(&g_seq_stats[1], n_chunks);
             atomicAdd(&g_seq_stats[2], n_vio);
+            atomicAdd(&g_seq_stats[3], n_rounds);
             atomicAdd(&g_seq_stats[4], cyc);
             atomicMax(&g_seq_stats[5], cyc);
             atomicMax(&g_seq_stats[6], n_chunks);
+            atomicMax(&g_seq_stats[7], max_m);
+            for (int k = 0; k < 16; ++k) atomicAdd(&g_seq_stats[8 + k], ph[k]);
+            if (n_chunks >= 20) {  // the hot relations alone
+                for (int k = 0; k < 16; ++k) atomicAdd(&g_seq_stats[24 + k], ph[k]);
+                atomicAdd(&g_seq_stats[40], n_chunks);
+                atomicAdd(&g_seq_stats[41], 1ull);
+                atomicAdd(&g_seq_stats[42], n_vio);
+            }
         }
-        if (l == 0 && n_rounds) atomicAdd(&g_seq_stats[3], n_rounds);
+    }
+}
+
+// The pair records of the batch's violators: G (left there by the chain kernel)
+// -> da = -lr W G with the relation's final matrix (transr/trainer.cpp:59-60,
+// first order in lr the same as the matrix at the pair's chunk).  The records
+// are the update slots of active samples with pflag set (4 B of them) and the
+// relations whose (entity[r], r) record carries this batch's stamp.  One wave a
+// record: lane i holds G_i, da_j = sum_i W[j][i] G_i by wave reductions.
+template <typename T>
+__global__ __launch_bounds__(256) void transr_cons_da_kernel(RParArgs a, RParBufs<T> bf) {
+    const int n = a.n, ld = a.ld, l = lane_id();
+    const int nwaves = (int)(gridDim.x * blockDim.x) >> 6;
+    const int nrec = 4 * a.B + a.nr;
+    for (int q = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); q < nrec; q += nwaves) {
+        int r;
+        T* row;
+        if (q < 4 * a.B) {
+            if (!a.act[q >> 2] || !bf.pflag[q]) continue;
+            r = a.rels[a.si[q >> 2]];
+            row = bf.pair + (int64_t)q * ld;
+        } else {
+            r = q - 4 * a.B;
+            if (bf.relpair_stamp[r] != bf.stamp) continue;
+            row = bf.relpair + (int64_t)r * ld;
+        }
+        const T gi = l < n ? row[l] : T(0);
+        const T* W = bf.W + (int64_t)r * n * ld;
+        T da = T(0);
+        for (int j = 0; j < n; ++j) {
+            const T s = wave_sum(l < n ? W[(int64_t)j * ld + l] * gi : T(0));
+            if (l == j) da = s;
+        }
+        if (l < n) row[l] = -(T)a.lr * da;
     }
 }
 

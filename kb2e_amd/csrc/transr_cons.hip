@@ -43,41 +43,33 @@ const void* cons_fn(int n) {
     return kernel_fn<T>(kCons, n);
 }
 
-template <typename T, int C>
-const void* seq_fn(int n) {
-    switch (rm_np(n)) {
-        case 16: return (const void*)transr_cons_seq_kernel<T, 16, C>;
-        case 32: return (const void*)transr_cons_seq_kernel<T, 32, C>;
-        case 48: return (const void*)transr_cons_seq_kernel<T, 48, C>;
-        case 64: return (const void*)transr_cons_seq_kernel<T, 64, C>;
-    }
-    throw std::runtime_error("transRNorm chunk kernel: n > 64");
+template <int... KS>
+const void* chain_table(int ks, std::integer_sequence<int, KS...>) {
+    const void* tab[] = {(const void*)transr_cons_chain_kernel<double, KS + 1>...};
+    return tab[ks - 1];
 }
 
-template <typename T>
-const void* seq_fn(int n, int C) {
-    return C == 64 ? seq_fn<T, 64>(n) : C == 16 ? seq_fn<T, 16>(n) : seq_fn<T, 32>(n);
+const void* chain_fn(int n) {
+    if (!cons_wave_supported(n)) throw std::runtime_error("transRNorm chain kernel: n > 64");
+    return chain_table((n + 3) / 4, std::make_integer_sequence<int, 16>{});
 }
 
 }  // namespace
 
-size_t cons_seq_setup(int n, int C, int esize) {
-    const size_t lds = esize == 8 ? seq_lds<double>(n, C) : seq_lds<float>(n, C);
-    HIPCHK(hipFuncSetAttribute(esize == 8 ? seq_fn<double>(n, C) : seq_fn<float>(n, C),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+size_t cons_seq_setup(int n) {
+    const size_t lds = chain_lds<double>(n);
+    HIPCHK(hipFuncSetAttribute(chain_fn(n), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     return lds;
 }
 
-template <typename T>
-void cons_seq_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, int C, size_t lds, hipStream_t stream) {
+void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, int grid, size_t lds, hipStream_t stream) {
     RParArgs aa = a;
-    RParBufs<T> bb = bf;
+    RParBufs<double> bb = bf;
     void* args[] = {&aa, &bb};
-    HIPCHK(hipLaunchKernel(seq_fn<T>(a.n, C), dim3(grid), dim3(kSeqThreads), args, lds, stream));
+    HIPCHK(hipLaunchKernel(chain_fn(a.n), dim3(grid), dim3(kChainThreads), args, lds, stream));
+    const int da_grid = (int)std::min<int64_t>(2048, ((int64_t)4 * a.B + a.nr + 3) / 4);
+    HIPCHK(hipLaunchKernel((const void*)transr_cons_da_kernel<double>, dim3(da_grid), dim3(256), args, 0, stream));
 }
-
-template void cons_seq_launch<double>(const RParArgs&, const RParBufs<double>&, int, int, size_t, hipStream_t);
-template void cons_seq_launch<float>(const RParArgs&, const RParBufs<float>&, int, int, size_t, hipStream_t);
 
 bool cons_wave_supported(int n) { return n >= 1 && n <= 64; }
 
@@ -122,9 +114,9 @@ template void grad_wave_launch<float>(const RParArgs&, const RParBufs<float>&, i
 template void cons_wave_launch<double>(const RParArgs&, const RParBufs<double>&, int, size_t, hipStream_t);
 template void cons_wave_launch<float>(const RParArgs&, const RParBufs<float>&, int, size_t, hipStream_t);
 
-void cons_seq_take_stats(unsigned long long (&st)[8]) {
+void cons_seq_take_stats(unsigned long long (&st)[64]) {
     HIPCHK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_seq_stats), sizeof(st)));
-    unsigned long long z[8] = {};
+    unsigned long long z[64] = {};
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_seq_stats), z, sizeof(z)));
 }
 

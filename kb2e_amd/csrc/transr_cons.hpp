@@ -26,15 +26,15 @@ void proj_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, hipStr
 // (kernels_transr_wave.hpp); needs bf.x, bf.d and the hinge decisions in place.
 template <typename T>
 void grad_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, hipStream_t stream);
-// transRNorm per relation in chunks of C pairs (kernels_transr_seq.hpp; n <= 64,
-// C = 16, 32 or 64): dynamic LDS bytes (and the kernels' limit raised to it), launch
-// (one workgroup per tile of the batch; a relation's first tile does the work).
-size_t cons_seq_setup(int n, int C, int esize);
-template <typename T>
-void cons_seq_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, int C, size_t lds, hipStream_t stream);
+// transRNorm per relation as a chain of 16-pair chunks (kernels_transr_seq.hpp; FP64,
+// n <= 64): dynamic LDS bytes (and the kernel's limit raised to it); launch of the chain
+// (one workgroup per tile of the batch; a relation's first tile does the work) and of
+// the pair records' kernel after it.
+size_t cons_seq_setup(int n);
+void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, int grid, size_t lds, hipStream_t stream);
 // The chunk kernel's counters (relations, chunks, violators, rounds, cycles sum / max,
 // most chunks of a relation), reset.
-void cons_seq_take_stats(unsigned long long (&st)[8]);
+void cons_seq_take_stats(unsigned long long (&st)[64]);
 // Adds the kernel's round statistics (g_rpar_rounds layout) to st and resets them.
 void cons_wave_take_stats(unsigned long long (&st)[16]);
 

@@ -184,19 +184,25 @@ def transr_norm_rounds(p, a0, K0, Q0, eps, max_iter=256):
     in eps along w (exact for m <= 2, geometric for long runs), so
     |p_t|^2 = rho^2t Q0 + eps^2 t^2 rho^(2t-2) |w|^2 and
     G = 2 (S0 p - eps S1 w), S0 = sum rho^t, S1 = sum t rho^(t-1).  Returns (G, m)."""
-    v = K0 @ p + (a0 @ a0) * p
-    kappa = (p @ v) / Q0
+    s0 = a0 @ a0
+    V = K0 @ p
+    pp, pV, VV = p @ p, p @ V, V @ V
+    v = V + s0 * p
+    pv, vv = pV + s0 * pp, VV + 2.0 * s0 * pV + s0 * s0 * pp   # p.v, |v|^2 (as the kernel sums them)
+    kappa = pv / pp
     w = v - kappa * p
-    w2 = w @ w
+    w2 = max(vv - kappa * pv, 0.0)
     rho = 1.0 - eps * kappa
+
+    e2w = eps * eps * w2
     m, S0, S1, rt, rtm1 = 0, 0.0, 0.0, 1.0, 0.0  # rt = rho^t, rtm1 = rho^(t-1) (0 at t = 0)
-    while m < max_iter and rt * rt * Q0 + eps * eps * m * m * rtm1 * rtm1 * w2 > 1.0:
+    while m < max_iter and rt * rt * pp + e2w * m * m * rtm1 * rtm1 > 1.0:
         S0 += rt
         S1 += m * rtm1
         m += 1
         rtm1 = rt
         rt *= rho
-    return 2.0 * (S0 * p - eps * S1 * w), m
+    return 2.0 * (S0 + eps * S1 * kappa) * p - 2.0 * eps * S1 * v, m
 
 
 def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, relpair=True, max_iter=256,
@@ -225,7 +231,7 @@ def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, 
     before its own last update are followed by a unit norm, those of its last
     update (or of (entity'[r], r) when no update touches the row) are not.
     Per violator the rounds in closed form (transr_norm_rounds, K0 = W'^T W');
-    da = -lr W_c G, W_c -= lr a G^T.
+    W_c -= lr a G^T, and da = -lr W G with the relation's final matrix.
 
     cons = "seq" (probe only, tools/probe_compat_parallel.py): the reference's
     own loop (oracle/orc.c transr_norm) on each pair in order, on the evolving
@@ -252,7 +258,8 @@ def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, 
     W0 = W.copy()
     E1 = ent.copy()
     if cons.startswith("chunk"):
-        C = int(cons[5:])
+        flags = cons[5:].lstrip("0123456789")  # probe only: "r" renormalise the rows at every chunk
+        C = int(cons[5:len(cons) - len(flags)])
         eps = 2.0 * rate
         # the last active update touching every entity (its unit norm in the
         # reference comes after every transRNorm shrink of earlier updates)
@@ -271,9 +278,12 @@ def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, 
             Wc = W0[rr].copy()
             K0 = Wc.T @ Wc
             changed = False
-            chunks = [head[c0:c0 + C] for c0 in range(0, len(head), C)] + ([tail] if tail else [])
+            recs = []  # (entity, post, G): da = -lr W G with the relation's final matrix
+            chunks = [head[c0:c0 + C] for c0 in range(0, len(head), C)]
+            first_tail = len(chunks)  # the last update's pairs: chunks of their own (C = 1: one by one)
+            chunks += [tail[c0:c0 + C] for c0 in range(0, len(tail), C)]
             for ci, chunk in enumerate(chunks):
-                if tail and ci == len(chunks) - 1 and changed:
+                if changed and (ci == first_tail or "r" in flags):
                     # the relation's last update renormalises the rows (transr/trainer.cpp:178-180):
                     # only its own shrinks outlive the batch
                     Wc = Wc / np.sqrt((Wc ** 2).sum(1, keepdims=True))
@@ -285,7 +295,7 @@ def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, 
                     e, key = chunk[k]
                     G, m = transr_norm_rounds(P[k], A[k], K0, Q0[k], eps, max_iter)
                     post = (e not in last_upd) if key is None else last_upd.get(e) == key
-                    (dE_post if post else dE_pre)[e] += -rate * (Wc @ G)
+                    recs.append((e, post, G))
                     dW -= rate * np.outer(A[k], G)
                     changed = True
                     if stats is not None:
@@ -295,6 +305,8 @@ def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, 
                     stats["pairs"] = stats.get("pairs", 0) + len(chunk)
                 Wc = Wc + dW
             W[rr] = Wc
+            for e, post, G in recs:
+                (dE_post if post else dE_pre)[e] += -rate * (Wc @ G)
         pre = np.nonzero(np.any(dE_pre != 0, axis=1))[0]
         ent[pre] += dE_pre[pre]
         ent[pre] /= np.sqrt((ent[pre] ** 2).sum(1, keepdims=True))

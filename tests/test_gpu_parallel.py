@@ -84,11 +84,12 @@ def test_transe_parallel_deterministic():
 
 def _cons_form(dim, mfma):
     """The transRNorm form the engine runs (engine_transr_parallel.inc): the
-    per-relation chunk kernel on the matrix-core path for n <= 64, unless
-    KB2E_RPAR_CONS picks the Jacobi tile / wave kernels."""
+    per-relation sequential kernel (every pair against the matrix the earlier
+    ones left) on the matrix-core path for n <= 64, unless KB2E_RPAR_CONS picks
+    the Jacobi tile / wave kernels."""
     ck = os.environ.get("KB2E_RPAR_CONS", "")
     if mfma and dim <= 64 and ck not in ("tile", "jacobi"):
-        return "chunk" + os.environ.get("KB2E_RPAR_SEQ_CHUNK", "32")
+        return "chunk1"
     return "jacobi"
 
 
@@ -143,13 +144,13 @@ def test_transr_parallel_cons_tile_kernel(dim, distance, St, compat, monkeypatch
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, distance=distance, compat=compat)
 
 
-@pytest.mark.parametrize("chunk", ["16", "64"])
-@pytest.mark.parametrize("dim,St,compat", [(20, 8, False), (50, 4, True)])
-def test_transr_parallel_chunk_sizes(dim, St, compat, chunk, monkeypatch):
-    """The per-relation transRNorm kernel with chunks of 16 and 64 pairs (32 is
-    the default): relations of the tiny set hold ~90 pairs a batch, so several
-    chunks, each seeing the matrix the earlier ones left."""
-    monkeypatch.setenv("KB2E_RPAR_SEQ_CHUNK", chunk)
+@pytest.mark.parametrize("dim,St,compat", [(20, 8, False), (50, 4, True), (64, 2, True), (17, 8, False), (18, 8, False),
+                                            (49, 8, False), (33, 4, True)])
+def test_transr_parallel_chain_widths(dim, St, compat, monkeypatch):
+    """The per-relation sequential transRNorm kernel (kernels_transr_seq.hpp) at
+    one to four column slices (n = 17 .. 64): relations of the tiny set hold ~90
+    pairs a batch, so several 32-pair chunks and several violators a chunk, each
+    pair against the matrix the earlier ones left."""
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=compat)
 
 
@@ -210,7 +211,9 @@ def test_transr_parallel_independent_of_tile_size(monkeypatch):
 
 
 def test_transr_parallel_fp32_close(monkeypatch):
-    """FP32 tables: hinge decisions flip at the margin, so statistics, not elements."""
+    """FP32 tables: hinge decisions flip at the margin, so statistics, not elements.
+    (Both on the Jacobi transRNorm: the chunked chain is FP64 only.)"""
+    monkeypatch.setenv("KB2E_RPAR_CONS", "jacobi")
     ds = tiny()
     out = {}
     for prec in (64, 32):
