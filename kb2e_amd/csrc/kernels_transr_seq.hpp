@@ -117,6 +117,24 @@ __device__ __forceinline__ int transr_rounds(T Q0, T w2, T eps, T rho, T& S0, T&
     return m;
 }
 
+// transr_rounds for a violator (Q0 > 1: round 0 always runs), from round 1
+template <typename T>
+__device__ __forceinline__ int transr_rounds_violator(T Q0, T w2, T eps, T rho, T& S0, T& S1) {
+    const T e2w = eps * eps * w2;
+    T rt = rho, rtm1 = T(1);  // rho^t, rho^(t-1) at t = 1
+    S0 = T(1);
+    S1 = T(0);
+    int m = 1;
+    while (m < kRParMaxIter && rt * rt * Q0 + e2w * (T)m * (T)m * rtm1 * rtm1 > T(1)) {
+        S0 += rt;
+        S1 += (T)m * rtm1;
+        rtm1 = rt;
+        rt *= rho;
+        ++m;
+    }
+    return m;
+}
+
 // KS = ceil(n / 4): the live k-steps of a contraction over n, a compile-time
 // count so that the MFMA chains are straight-line code (no per-step branches)
 template <typename T, int KS>
@@ -206,6 +224,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
     __syncthreads();
     const int run = misc[5], has_rel = misc[3], g_tail = misc[4], n_tail = misc[6];
     bool have_k0 = false, changed = false;
+    T k0c[4 * KS];  // wave 0: K0's column l (the violators' V rows), loaded once K0 is made
     tick(0);
     int chunk_no = 0;  // chunks so far (row buffer parity)
     // windows of at most kSeqMaxTiles tiles and kChainList - 1 pairs (FB15k's hottest
@@ -293,8 +312,12 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
             }
         };
         __syncthreads();
-        load_rows(0, chunk_end(0));
-        store_rows(chunk_no & 1);
+        {
+            const int e0 = chunk_end(0);
+            load_rows(0, e0);
+            store_rows(chunk_no & 1);
+            load_rows(e0, e0 < npairs ? chunk_end(e0) : e0);  // the second chunk's rows in flight
+        }
         __syncthreads();
         for (int base = 0; base < npairs; ++chunk_no) {
             const int nbase = chunk_end(base);
@@ -302,7 +325,6 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
             const int nrt = cc > 16 ? 2 : 1;  // row tiles of the chunk
             const T* A = Abuf + (chunk_no & 1) * R * L;
             ++n_chunks;
-            load_rows(nbase, nbase < npairs ? chunk_end(nbase) : nbase);  // next chunk's rows in flight
             if (base == tail_start && changed) {
                 // the relation's last update renormalises the rows before its own pairs'
                 // shrinks (transr/trainer.cpp:178-180): row sums over the slices, then each
@@ -326,11 +348,13 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
             // Phase A, all waves: P = A W_c and the Gram matrix A A^T of the chunk, 16 x 16
             // MFMA tiles dealt round the waves; |p|^2 partials per column slice.
             {
-                const int ntiles = nrt * NB + nrt * nrt;
+                // Gram tiles (0, 0), (1, 0), (1, 1): only a_j . a_v with j > v is read
+                const int ntiles = nrt * NB + (nrt == 2 ? 3 : 1);
                 for (int tl = w; tl < ntiles; tl += kChainThreads / kWave) {
                     const bool gram = tl >= nrt * NB;
-                    const int rt = gram ? (tl - nrt * NB) / nrt : tl / NB;
-                    const int cb = gram ? (tl - nrt * NB) % nrt : tl % NB;
+                    const int gi = tl - nrt * NB;
+                    const int rt = gram ? (gi == 0 ? 0 : 1) : tl / NB;
+                    const int cb = gram ? (gi == 2 ? 1 : 0) : tl % NB;
                     typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
                     T av[KS], bv[KS];
 #pragma unroll
@@ -357,6 +381,15 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
                         }
                     }
                 }
+            }
+            // the next chunk's rows (loaded a chunk ago) into the other buffer, then the
+            // rows of the chunk after it in flight for a whole chunk (before wave 0's
+            // record stores: waiting for a load waits for every global access issued
+            // before it)
+            store_rows((chunk_no & 1) ^ 1);  // (zeros past the window's last chunk: unread)
+            {
+                const int n2 = nbase < npairs ? chunk_end(nbase) : nbase;
+                load_rows(n2, n2 < npairs ? chunk_end(n2) : n2);
             }
             __syncthreads();  // B1
             tick(2);
@@ -387,6 +420,11 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
                     }
                 }
                 __syncthreads();
+                if (w == 0) {
+                    const int cK = l < NP ? l : 0;
+#pragma unroll
+                    for (int i = 0; i < 4 * KS; ++i) k0c[i] = K0[i * L + cK];
+                }
             }
             tick(3);
             // Phase B, wave 0: the pairs in order, each against the matrix the earlier
@@ -404,40 +442,32 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
                     const int v = __builtin_ctzll(cand);
                     const int c = l;  // column
                     const T pv = c < NP ? P[v * L + c] : T(0);
-                    const T av = c < NP ? A[v * L + c] : T(0);
-                    // V[c] = sum_i p_v[i] K0[i][c], four chains
+                    // V[c] = sum_i p_v[i] K0[i][c] (K0's column c in lane c's registers), four chains
                     T vv4[4] = {T(0), T(0), T(0), T(0)};
-                    const int cK = c < NP ? c : 0;
 #pragma unroll
                     for (int t = 0; t < KS; ++t)
 #pragma unroll
-                        for (int u = 0; u < 4; ++u)
-                            vv4[u] = fma(P[v * L + 4 * t + u], K0[(4 * t + u) * L + cK], vv4[u]);
+                        for (int u = 0; u < 4; ++u) vv4[u] = fma(P[v * L + 4 * t + u], k0c[4 * t + u], vv4[u]);
                     const T Vc = c < n ? (vv4[0] + vv4[1]) + (vv4[2] + vv4[3]) : T(0);
                     tick(7);
-                    T s3[3] = {pv * Vc, Vc * Vc, av * av};
-                    wave_sums<T, 3>(s3);
+                    T s2[2] = {pv * Vc, Vc * Vc};
+                    wave_sums<T, 2>(s2);
                     tick(8);
                     const T pp = readlane_f(q, v);
-                    const T pV = s3[0], VV = s3[1], aa = s3[2];
+                    const T pV = s2[0], VV = s2[1], aa = Gm[v * LG + v];  // |a_v|^2: the Gram diagonal
                     const T pvd = pV + aa * pp, vvd = VV + T(2) * aa * pV + aa * aa * pp;
                     const T kappa = pvd / pp;
                     const T w2t = vvd - kappa * pvd;
                     const T w2 = w2t > T(0) ? w2t : T(0);
                     const T rho = T(1) - eps * kappa;
                     T S0, S1;
-                    const int m = transr_rounds(pp, w2, eps, rho, S0, S1);
+                    const int m = transr_rounds_violator(pp, w2, eps, rho, S0, S1);
                     n_rounds += (unsigned long long)m;
                     max_m = max_m > (unsigned long long)m ? max_m : (unsigned long long)m;
                     const T cpf = T(2) * (S0 + eps * S1 * kappa), cvf = T(2) * eps * S1;
                     const T g = c < n ? cpf * pv - cvf * (Vc + aa * pv) : T(0);
                     tick(9);
-                    if (c < NP) P[v * L + c] = g;  // the violator's row now holds G
-                    {  // the pair record (da = -lr W G made later)
-                        const int sl = ps[base + v];
-                        T* dst = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
-                        if (c < n) dst[c] = g;
-                    }
+                    if (c < NP) P[v * L + c] = g;  // the violator's row now holds G (records after B2)
                     tick(10);
                     // the later pairs: P[j] -= lr (a_j . a_v) g, |p_j|^2 afresh (lane j: half
                     // l >> 5 of the columns)
@@ -490,8 +520,19 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
             __syncthreads();  // B2
             tick(5);
             if (anyv) {
-                // W_c[:, slice] -= lr sum_v A[v]^T G[v] over the chunk's violators
                 const uint32_t vmask = (uint32_t)misc[1];
+                {  // the violators' pair records G (da = -lr W G made later), a wave each
+                    uint32_t mm = vmask;
+                    for (int k = 0; k < w && mm; ++k) mm &= mm - 1;
+                    while (mm) {
+                        const int v = __builtin_ctz(mm);
+                        const int sl = ps[base + v];
+                        T* dst = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
+                        if (l < n) dst[l] = P[v * L + l];
+                        for (int k = 0; k < 4 && mm; ++k) mm &= mm - 1;
+                    }
+                }
+                // W_c[:, slice] -= lr sum_v A[v]^T G[v] over the chunk's violators
                 if (vmask) changed = true;
                 if (mine) {
                     T wv[KS];
@@ -507,8 +548,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
                     for (int t = 0; t < KS; ++t) Wc[(kq + 4 * t) * L + col] = wv[t];
                 }
             }
-            store_rows((chunk_no & 1) ^ 1);  // (zeros past the window's last chunk: unread)
-            __syncthreads();  // B3: the next chunk's rows and W_c
+            __syncthreads();  // B3: W_c
             tick(6);
             base = nbase;
         }
