@@ -23,6 +23,12 @@ transr/transr.cpp:20-25) does not learn under the reference's own algorithm:
 its ORDERED run ends *below* the seed tables' Hits@10 (1.1 % after 150 epochs
 against 2.5 % for the seed alone on this set), so only the schedule delta is
 asserted for it.
+
+TransR runs at the north-star width n = 50, and the loss trajectory is bounded
+too: the mean loss of the last 10 epochs within LOSS_TOL_REL of ORDERED's.  On
+the FB15k-shaped set the ORDERED seed envelope (5 glibc seeds) spans +-3.6 %
+around its mean and PARALLEL sits 2.6 % below it
+(profiles/seed_envelope_r17_fb15k_R_compat.jsonl, .._r18_.._parallel_seq.jsonl).
 """
 import pytest
 
@@ -33,6 +39,7 @@ pytestmark = pytest.mark.gpu
 
 HITS_TOL_PP = 0.5
 RANK_TOL_REL = 0.02
+LOSS_TOL_REL = 0.05
 
 
 @pytest.fixture(scope="module")
@@ -43,8 +50,8 @@ def ds():
 @pytest.mark.parametrize("model,dim,epochs,compat,learns", [
     ("E", 50, 300, True, True),
     ("H", 50, 300, True, True),
-    ("R", 32, 50, False, True),   # fixed energy
-    ("R", 32, 50, True, False),   # compat energy (the reference default)
+    ("R", 50, 50, False, True),   # fixed energy
+    ("R", 50, 50, True, False),   # compat energy (the reference default)
 ])
 def test_parallel_schedule_matches_reference_hits10(ds, model, dim, epochs, compat, learns):
     out = schedule_parity(ds, model, dim, epochs, seed_epochs=300, rate=0.001, method=1, batches=100, seed=7,
@@ -58,3 +65,7 @@ def test_parallel_schedule_matches_reference_hits10(ds, model, dim, epochs, comp
     assert abs(p["filtered_rank"] - o["filtered_rank"]) <= RANK_TOL_REL * o["filtered_rank"], out
     # same sample stream: the final epoch's hinge-active counts stay close
     assert abs(p["losses"][-1][2] - o["losses"][-1][2]) <= 0.05 * o["losses"][-1][2]
+    # and the loss trajectory: the last 10 epochs' mean loss
+    lo = sum(x[1] for x in o["losses"][-10:]) / 10
+    lp = sum(x[1] for x in p["losses"][-10:]) / 10
+    assert abs(lp - lo) <= LOSS_TOL_REL * lo, (lp, lo)
