@@ -1033,15 +1033,15 @@ void setup_buffers(kb2e_ctx* c) {
     const size_t es = (size_t)c->esize;
     c->ent.alloc((size_t)g.num_entities * c->ld * es);
     c->rel.alloc((size_t)g.num_relations * c->ld * es);
-    HIPCHK(hipMemset(c->ent.p, 0, c->ent.bytes));
-    HIPCHK(hipMemset(c->rel.p, 0, c->rel.bytes));
+    memset_sync(c->ent.p, 0, c->ent.bytes);
+    memset_sync(c->rel.p, 0, c->rel.bytes);
     if (g.model == KB2E_TRANSH) c->w_elems = (int64_t)g.num_relations * g.dim;
     if (g.model == KB2E_TRANSR) c->w_elems = (int64_t)g.num_relations * g.dim * g.dim;
     c->w.alloc((size_t)std::max<int64_t>(1, w_rows(c)) * c->ld * es);
-    HIPCHK(hipMemset(c->w.p, 0, c->w.bytes));
+    memset_sync(c->w.p, 0, c->w.bytes);
     if (g.model == KB2E_TRANSR) {  // committed matrices (start-of-batch snapshot)
         c->wsnap.alloc(c->w.bytes);
-        HIPCHK(hipMemset(c->wsnap.p, 0, c->wsnap.bytes));
+        memset_sync(c->wsnap.p, 0, c->wsnap.bytes);
     }
     c->device_bytes = (int64_t)(c->ent.bytes + c->rel.bytes + c->w.bytes);
 }
@@ -1115,7 +1115,7 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     if (g.distance != 0 || g.model == KB2E_TRANSR)
         c->xreal.alloc((size_t)c->B * 2 * c->ld * c->esize);
     c->stats.alloc((2 + 2 * kStatSlices) * 8);
-    HIPCHK(hipMemset(c->stats.p, 0, c->stats.bytes));
+    memset_sync(c->stats.p, 0, c->stats.bytes);
     if (g.model != KB2E_TRANSR && g.schedule == KB2E_SCHEDULE_PARALLEL) {
         const int64_t per_batch = c->B * c->slots;
         c->par_long_cap = (int32_t)(c->apply_long_min > 0 ? std::min<int64_t>(per_batch, per_batch / c->apply_long_min + 1)
@@ -1130,7 +1130,7 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     if (g.model == KB2E_TRANSR && g.schedule == KB2E_SCHEDULE_PARALLEL) setup_transr_parallel(c);
     if (g.model == KB2E_TRANSH && g.schedule == KB2E_SCHEDULE_PARALLEL) {
         c->hpar_orth.alloc((size_t)((c->B + 511) / 512) * 512);  // whole 8-byte words past B stay zero
-        HIPCHK(hipMemset(c->hpar_orth.p, 0, c->hpar_orth.bytes));
+        memset_sync(c->hpar_orth.p, 0, c->hpar_orth.bytes);
         c->rpar_St = 1 << 30;  // build_transr_tiles(c, false): relation segment ranges only
         c->rpar_ntiles.alloc((size_t)(nkeys + 1) * 4);
         c->rpar_rel_begin.alloc((size_t)c->nb * 4);

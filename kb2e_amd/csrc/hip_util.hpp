@@ -22,6 +22,13 @@ struct HipError : std::runtime_error {
                                    std::string(__FILE__) + ":" + std::to_string(__LINE__));       \
     } while (0)
 
+// hipMemset on the null stream, waited for: the engine's streams are
+// non-blocking, so a kernel or copy queued on them next does not order after it.
+inline void memset_sync(void* p, int v, size_t b) {
+    HIPCHK(hipMemset(p, v, b));
+    HIPCHK(hipStreamSynchronize(nullptr));
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -32,8 +39,12 @@ struct DevBuf {
         free();
         if (b == 0) b = 16;
         HIPCHK(hipMalloc(&p, b));
-        // zeroed: no kernel result may depend on what an earlier engine left in the heap
-        HIPCHK(hipMemset(p, 0, b));
+        // zeroed: no kernel result may depend on what an earlier engine left in the
+        // heap.  hipMemset runs on the null stream, which does not order against the
+        // engine's non-blocking streams: wait for it here, or an upload queued next
+        // on another stream (the filter table, the triples) can land before the
+        // zeros and be wiped.
+        memset_sync(p, 0, b);
         bytes = b;
     }
     void free() {

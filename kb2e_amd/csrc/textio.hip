@@ -451,7 +451,7 @@ int64_t parse_doubles(const char* text, int64_t len, int64_t count, double* out,
                 HIPCHK(hipMemcpy(out + sl[2 * q], &v, 8, hipMemcpyHostToDevice));
             }
             *slow_out += (int64_t)nslow;
-            HIPCHK(hipMemset(flags.p, 0, 8));
+            memset_sync(flags.p, 0, 8);
         }
         tokens += ntok;
         pos = end;
