@@ -162,6 +162,25 @@ def _ref_epoch_seconds(cmd, epochs, limit_s):
     return (stamps[last] - stamps[0]) / last, last
 
 
+def _ref_epoch_seconds_diff(cmd, epochs):
+    """Seconds per epoch of the reference binary on one core without a
+    terminal: wall time of an `epochs`-epoch run minus that of a 1-epoch run,
+    over epochs - 1 (data loading, init and epoch 0 cancel)."""
+    cpu = min(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+
+    def pin():
+        if cpu is not None:
+            os.sched_setaffinity(0, {cpu})
+
+    walls = []
+    for e in (1, epochs):
+        t0 = time.perf_counter()
+        subprocess.run(cmd + ["--epochs", str(e)], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                       stdin=subprocess.DEVNULL, preexec_fn=pin, check=True)
+        walls.append(time.perf_counter() - t0)
+    return (walls[1] - walls[0]) / (epochs - 1), epochs - 1
+
+
 def cpu_baseline(cfg_name, ds, seed_dir=None, budget_s=25.0):
     """The reference itself (oracle/_ref, compiled from the reference sources)
     on this host, single-threaded, on the same synthetic dataset; falls back to
@@ -181,11 +200,18 @@ def cpu_baseline(cfg_name, ds, seed_dir=None, budget_s=25.0):
                 # the same TransE seed files the GPU run read (transr/trainer.cpp:88-113)
                 cmd += ["--seeddatadir", seed_dir, "--seedmethod", "0"]
                 seed_note = f", seeded from the GPU run's TransE-init files ({SEED_EPOCHS} TransE epochs)"
-            per_epoch, timed = _ref_epoch_seconds(cmd, epochs, budget_s * 8)
+            try:
+                per_epoch, timed = _ref_epoch_seconds(cmd, epochs, budget_s * 8)
+                how = (f"mean time of epochs 1..{timed} from the timestamps of its Epoch lines (epoch 0 and init "
+                       f"excluded)")
+            except OSError:  # no pseudo-terminal on this host: two whole runs, differenced
+                per_epoch, timed = _ref_epoch_seconds_diff(cmd, epochs)
+                how = (f"(wall of a {epochs}-epoch run - wall of a 1-epoch run) / {timed} (init and epoch 0 "
+                       f"cancel)")
         return {"value": S / per_epoch, "unit": "triples/s", "cores": 1, "kind": "reference", **host_cpu(),
                 "sample": f"{os.path.basename(binary)} (compiled from the reference sources) on the same synthetic "
-                          f"{shape}-shaped data{seed_note}, 1 thread pinned to one core; mean time of epochs 1..{timed} "
-                          f"from the timestamps of its Epoch lines (epoch 0 and init excluded), {S} samples per epoch"}
+                          f"{shape}-shaped data{seed_note}, 1 thread pinned to one core; {how}, {S} samples per "
+                          f"epoch"}
     from oracle import orc  # CPU restatement (port) fallback
     m = orc.Model(model, dim, ds.num_entities, ds.num_relations, rate=rate, method=method, distance=distance,
                   batches=100)
