@@ -61,6 +61,7 @@ CONFIGS = {
 }
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 SEED_EPOCHS = 100  # TransE epochs behind the TransR seed tables ("TransE-init")
+LATE_EPOCH = 50  # the steady-state epoch timed beside the K batches (bench.py --late-epoch)
 
 
 def host_cpu():
@@ -238,7 +239,7 @@ def phase_bytes(model, n, s, a):
     return score_b, fold_b
 
 
-def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, seed_tabs=None):
+def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, seed_tabs=None, late=0):
     """Train `warmup` then time `steps` batches of one schedule; returns a dict."""
     from kb2e_amd.engine import Engine
 
@@ -323,6 +324,15 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
         eng.profile(0)
         to_epoch_start()
         epoch_s = timed(batches)
+    late_s = None
+    if late and not args.no_epoch:
+        # steady state: train on to `late` epochs, then time the next whole epoch
+        # (hinge-active samples fall and TransH's orthogonality list grows with training)
+        to_epoch_start()
+        if run.pos < late * batches:
+            run(late * batches - run.pos)
+        eng.synchronize()
+        late_s = timed(batches)
     eng.close()
     samples = steps * B
     if dist is not None:
@@ -362,9 +372,20 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             epoch_s = float(t[0])
         epoch_rec = {"value": batches * B * world / epoch_s, "ms": epoch_s * 1e3, "batches": batches}
+    late_rec = None
+    if late_s is not None:
+        if dist is not None:
+            import torch
+
+            t = torch.tensor([late_s], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            late_s = float(t[0])
+        late_rec = {"value": batches * B * world / late_s, "ms": late_s * 1e3, "batches": batches,
+                    "epoch_index": late}
     return {
         "value": samples / elapsed, "ms_per_step": elapsed / steps * 1e3, "B": B, "batches": batches,
         "epoch": epoch_rec,
+        "late_epoch": late_rec,
         "active_fraction": a,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": dominant,
@@ -386,6 +407,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-epoch", action="store_true", help="skip the whole-epoch timing")
     ap.add_argument("--seed-epochs", type=int, default=SEED_EPOCHS)
+    ap.add_argument("--late-epoch", type=int, default=LATE_EPOCH,
+                    help="also time the whole epoch with this index (steady state); 0: skip")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -410,7 +433,8 @@ def main():
     if model == "R" and shape != "k5":
         # every rank draws the same seed (fixed glibc seed), no broadcast needed
         seed_tabs = transe_seed(ds, dim, seed_tmp.name, epochs=args.seed_epochs, device=local if world > 1 else 0)
-    main_run = measure(args, args.schedule, ds, train, rank, world, local, dist, args.steps, args.warmup, seed_tabs)
+    main_run = measure(args, args.schedule, ds, train, rank, world, local, dist, args.steps, args.warmup, seed_tabs,
+                       late=args.late_epoch if shape != "k5" else 0)
     other = "ordered" if args.schedule == "parallel" else "parallel"
     other_run = None
     if not args.only:
@@ -448,7 +472,7 @@ def main():
         "timing": "K batches from an epoch boundary (epoch sampling commit + index build inside)",
     }
     out["schedules"] = {args.schedule: {"value": main_run["value"], "ms_per_step": main_run["ms_per_step"],
-                                        "epoch": main_run["epoch"]}}
+                                        "epoch": main_run["epoch"], "late_epoch": main_run["late_epoch"]}}
     if other_run is not None:
         out["schedules"][other] = {"value": other_run["value"], "ms_per_step": other_run["ms_per_step"],
                                    "epoch": other_run["epoch"], "active_fraction": other_run["active_fraction"],

@@ -151,6 +151,8 @@ struct kb2e_ctx {
     int32_t par_long_cap = 1, apply_grid = 256;
     DevBuf par_long_list, par_long_count;  // per epoch: long segments of every batch
     DevBuf hpar_orth;                      // PARALLEL TransH: orthogonality flags per sample
+    DevBuf hpar_tag;                       // PARALLEL TransH: per entity, the relations its flagged pairs have
+    uint32_t hpar_stamp = 0;
     // PARALLEL schedule: per-event records in sorted order (kernels_transe.hpp EventRecs)
     DevBuf ev_iota, ev_slot_sorted, ev_inv, seg_row, ev_meta, ev_words;
     // PARALLEL TransR (kernels_transr_parallel.hpp)
@@ -1131,6 +1133,7 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     if (g.model == KB2E_TRANSH && g.schedule == KB2E_SCHEDULE_PARALLEL) {
         c->hpar_orth.alloc((size_t)((c->B + 511) / 512) * 512);  // whole 8-byte words past B stay zero
         memset_sync(c->hpar_orth.p, 0, c->hpar_orth.bytes);
+        c->hpar_tag.alloc((size_t)c->cfg.num_entities * 8);  // zeroed: stamp 0 is never a batch's
         c->rpar_St = 1 << 30;  // build_transr_tiles(c, false): relation segment ranges only
         c->rpar_ntiles.alloc((size_t)(nkeys + 1) * 4);
         c->rpar_rel_begin.alloc((size_t)c->nb * 4);
@@ -1661,9 +1664,9 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
                         q[3], q[7], q[0] ? (double)q[4] / (double)q[0] : 0.0, q[5]);
                 fprintf(stderr, "rpar_cons chunk phases (prologue, issue+renorm, P+Gram+B1, K0, violators, B2, "
                         "W update+rows+B3; violator: V, sums, rounds, record, update):");
-                for (int k = 8; k < 20; ++k) fprintf(stderr, " %llu", q[k]);
+                for (int k = 8; k < 24; ++k) fprintf(stderr, " %llu", q[k]);
                 fprintf(stderr, "; hot relations (%llu, %llu chunks, %llu violators):", q[41], q[40], q[42]);
-                for (int k = 24; k < 36; ++k) fprintf(stderr, " %llu", q[k]);
+                for (int k = 24; k < 40; ++k) fprintf(stderr, " %llu", q[k]);
                 fprintf(stderr, "\n");
             }
             if (c->rpar_cons_wave)

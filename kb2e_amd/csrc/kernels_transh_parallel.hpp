@@ -45,7 +45,33 @@ struct HParArgs {
     T* rel;
     T* w;
     uint8_t* orth_mask;       // [B] violating (update, row) pairs of each sample, bits u * 3 + {r, h, t}
+    unsigned long long* ent_tag;  // [ne] stamp << 32 | multi << 31 | relation of the entity's flagged pairs
+    uint32_t stamp;           // this batch's tag stamp (never 0)
 };
+
+// The flagged entity rows' relations this batch: the first relation a row is
+// flagged under, and a mark once a second one shows up (one CAS loop).
+template <typename T>
+__device__ __forceinline__ void orth_tag_entity(HParArgs<T> a, int e, int r) {
+    unsigned long long* p = a.ent_tag + e;
+    const unsigned long long mine = ((unsigned long long)a.stamp << 32) | (unsigned)r;
+    unsigned long long old = *p;
+    for (;;) {
+        unsigned long long nv;
+        if ((uint32_t)(old >> 32) != a.stamp) nv = mine;
+        else if ((old & 0x80000000ull) || (uint32_t)(old & 0x7fffffffu) == (uint32_t)r) return;
+        else nv = old | 0x80000000ull;
+        const unsigned long long prev = atomicCAS(p, old, nv);
+        if (prev == old) return;
+        old = prev;
+    }
+}
+
+// an entity row flagged under more than one relation this batch (its tag was set by this batch)
+template <typename T>
+__device__ __forceinline__ bool orth_shared(HParArgs<T> a, int e) {
+    return (a.ent_tag[e] & 0x80000000ull) != 0;
+}
 
 // One NWV-wave workgroup per relation segment of the batch: waves sum chunks
 // of its events, partial sums combined in wave order, wave 0 applies.  The
@@ -175,7 +201,12 @@ __global__ __launch_bounds__(256) void transh_orth_check_kernel(HParArgs<T> a) {
             for (int k = 0; k < kVec; ++k) x += W.v[cc][k] * A.v[cc][k];
         if (wave_sum(x) > T(0.1)) mask |= 1u << q;
     }
-    if (l == 0) a.orth_mask[kk] = (uint8_t)mask;
+    if (l == 0) {
+        a.orth_mask[kk] = (uint8_t)mask;
+        const int ids[6] = {r, h, t, r, nh, nt};
+        for (int q = 1; q < 6; ++q)
+            if (q != 3 && ((mask >> q) & 1u)) orth_tag_entity(a, ids[q], r);
+    }
 }
 
 // One wave, samples in order: the reference's normOrth (common/utils.cpp:79-111,
@@ -290,5 +321,81 @@ __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
     if (wid >= 0) row_store_sc1(W, a.w + (int64_t)wid * a.ld, a.n);
     drain_stores();
 }
+
+// normOrth, first pass (oracle/parallel.py transh_parallel_batches): one wave per
+// relation segment of the batch, its samples in order, on the pairs only this
+// relation touches -- the relation row r' and the entity rows flagged under r
+// alone -- with w_r in registers; those bits are cleared, so the one-wave
+// serial pass (transh_orth_fix_kernel) then runs only the entity rows that
+// several relations flagged.  The relations' passes touch disjoint rows.
+template <typename T, int CH>
+__global__ __launch_bounds__(256) void transh_orth_rel_kernel(HParArgs<T> a) {
+    const int s = a.rel_begin[a.batch] + (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (s >= a.batch_seg[a.batch + 1]) return;
+    const int l = lane_id();
+    const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
+    const int r = a.seg_row[s] - a.ne;
+    RowReg<T, CH> W;
+    bool have_w = false;
+    PendingRows pend;  // a row stored earlier is drained before it is loaded again
+    for (int base = p0; base < p1; base += kWave) {
+        // lane-parallel: this lane's sample (an active sample's first update event),
+        // its flagged rows' ids and which of them only this relation touches
+        const int p = base + l;
+        uint32_t mine = 0;
+        int ids[6] = {r, 0, 0, r, 0, 0};
+        if (p < p1) {
+            const int32_t meta = a.meta[p];
+            const int xrow = meta >> 4;
+            if (((meta & 3) - 1) != 0 && (xrow & 1) == 0) {
+                const int kk = xrow >> 1;
+                const uint32_t bits = a.orth_mask[kk];
+                if (bits) {
+                    const int i0 = a.si[kk], j = a.sj[kk];
+                    const bool sd = a.side[kk];
+                    const int h = a.heads[i0], t = a.tails[i0];
+                    ids[1] = h;
+                    ids[2] = t;
+                    ids[4] = sd ? h : j;
+                    ids[5] = sd ? j : t;
+                    uint32_t keep = 0;
+#pragma unroll
+                    for (int q = 1; q < 6; ++q)
+                        if (q != 3 && ((bits >> q) & 1u) && orth_shared(a, ids[q])) keep |= 1u << q;
+                    mine = bits & ~keep;
+                    if (mine) a.orth_mask[kk] = (uint8_t)keep;
+                }
+            }
+        }
+        // serial, samples in order: normOrth on this relation's own rows, w_r in registers
+        uint64_t m = __ballot(mine != 0);
+        while (m) {
+            const int e = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t eb = (uint32_t)readlane_i32((int)mine, e);
+            int rid[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) rid[q] = readlane_i32(ids[q], e);
+            if (!have_w) {
+                row_load_sc1(W, a.w + (int64_t)r * a.ld, a.n);
+                have_w = true;
+            }
+            for (int q = 0; q < 6; ++q) {
+                if (!((eb >> q) & 1u)) continue;
+                T* row = (q == 0 ? a.rel : a.ent) + (int64_t)rid[q] * a.ld;
+                const int key = q == 0 ? -1 : rid[q];
+                RowReg<T, CH> A;
+                pend.before_load(key);
+                row_load_sc1(A, row, a.n);
+                orth_norm<T, CH>(A, W, a.n, (T)a.lr);
+                row_store_sc1(A, row, a.n);
+                pend.add(key);
+            }
+        }
+    }
+    if (have_w) row_store_sc1(W, a.w + (int64_t)r * a.ld, a.n);
+    drain_stores();
+}
+
 
 }  // namespace kb2e

@@ -1,0 +1,538 @@
+// kernels_transr_pipe.hpp -- the per-relation sequential transRNorm of the
+// PARALLEL TransR schedule (kernels_transr_seq.hpp explains the semantics:
+// every pair against the matrix the relation's earlier pairs left,
+// transr/trainer.cpp:35-64, :185-187; CPU model oracle/parallel.py
+// transr_constraint, cons="chunk1"), software-pipelined across chunks.
+//
+// transr_cons_chain_kernel spends a chunk of 32 pairs as: all four waves make
+// P = A W_c and the Gram matrix (MFMA), barrier, wave 0 walks the violators,
+// barrier, all waves fold the violators into W_c, barrier -- the projections
+// of a chunk wait for the previous chunk's walk.  Here the three other waves
+// make the NEXT chunk's projections while wave 0 walks the current one:
+//   X_{k+1} = A_{k+1} W_{k-1}                  (the matrix before chunk k's walk)
+//   C       = A_{k+1} A_k^T                    (cross Gram, next x current)
+//   P_{k+1} = X_{k+1} - lr C[:, vio_k] G_k     (chunk k's shrinks, W_k = W_{k-1} - lr A_k^T G_k)
+// so after the walk only a rank-|vio_k| correction, the W update and the next
+// chunk's |p|^2 sit between two walks.  The walk keeps the chunk's projection
+// rows in registers (lane j: half l >> 5 of row j & 31), so a violator's
+// rank-1 move of the later rows is FMAs on registers with the violator's G row
+// read as LDS broadcasts.  The relation's last-update chunk starts after W_c's
+// rows are renormalised: its projections are then made afresh (all waves).
+#pragma once
+
+#include "kernels_transr_cons.hpp"  // pair_sum32
+#include "kernels_transr_seq.hpp"
+
+namespace kb2e {
+
+constexpr int kPipeList = 1536;  // pairs of one relation a window (entity and slot lists in LDS)
+
+// LDS (elements of T): W_c [NP][L] | A [3][R][L] | P [2][R][L] (K0 [NP][L] in the
+// prologue) | Gram [2][R][LG] | cross Gram [R][LG] | |p|^2 partials [4][R] | row
+// partials [4][NP]; ints: pair entities, slots [kPipeList] each | pre
+// [kSeqMaxTiles + 1] | misc [8] | the chunk's violators [R]
+template <typename T>
+__host__ __device__ constexpr size_t pipe_lds(int n) {
+    return sizeof(T) * ((size_t)rm_np(n) * rm_ld(n) + 5 * (size_t)kChainRows * rm_ld(n) +
+                        3 * (size_t)kChainRows * (kChainRows + 1) + 4 * kChainRows + 4 * (size_t)rm_np(n)) +
+           sizeof(int) * (size_t)(2 * kPipeList + kSeqMaxTiles + 1 + 8 + kChainRows);
+}
+
+template <typename T, int KS>
+__global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArgs a, RParBufs<T> bf) {
+    using M = Mfma16<T>;
+    static_assert(sizeof(T) == 8, "the D-row / k-step identity below is the FP64 fragment layout");
+    constexpr int NB = (4 * KS + 15) / 16;  // column slices of 16
+    constexpr int NP = 16 * NB, L = NP + 2, R = kChainRows, LG = R + 1;
+    constexpr int NH = NP / 2;              // columns of a row half (walk registers)
+    static_assert(2 * R * L >= NP * L, "the K0 image borrows the two P buffers");
+    const int t0 = a.batch_t0[a.batch], t1 = a.batch_t0[a.batch + 1];
+    const int g0 = blockIdx.x;
+    if (t0 + g0 >= t1) return;
+    const int r = a.td_r[t0 + g0];
+    if (g0 > 0 && a.td_r[t0 + g0 - 1] == r) return;  // not the relation's first tile
+    const int n = a.n, ld = a.ld;
+    const int w = threadIdx.x >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
+    const bool mine = w < NB;  // this wave owns a column slice (K0, the W_c update)
+    const int col = 16 * w + l16;
+    const T lr = (T)a.lr;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* Wc = (T*)smem;
+    T* Abuf = Wc + NP * L;      // [3][R][L] entity rows of chunks k, k+1, k+2
+    T* Pbuf = Abuf + 3 * R * L;  // [2][R][L] projections (then the violators' G rows) of chunks k, k+1
+    T* Gbuf = Pbuf + 2 * R * L;  // [2][R][LG] Gram matrices A A^T of chunks k, k+1
+    T* Cx = Gbuf + 2 * R * LG;   // [R][LG] A_{k+1} A_k^T
+    T* qpart = Cx + R * LG;      // [4][R] |p_j|^2 partials of the column slices (next chunk)
+    T* rp = qpart + 4 * R;       // [4][NP] row partials of the tail renorm
+    int* pe = (int*)(rp + 4 * NP);
+    int* ps = pe + kPipeList;
+    int* pre = ps + kPipeList;
+    int* misc = pre + kSeqMaxTiles + 1;
+    int* vlist = misc + 8;  // the current chunk's violators in order (misc[2]: their count)
+    const long long ck0 = clock64();
+    unsigned long long n_chunks = 0, n_vio = 0, n_rounds = 0, max_m = 0;
+    unsigned long long ph[16] = {};
+    long long tq = ck0;
+    auto tick = [&](int k) {
+        if (bf.stats && threadIdx.x == 0) {
+            const long long t = clock64();
+            ph[k] += (unsigned long long)(t - tq);
+            tq = t;
+        }
+    };
+
+    // W'_r, zero padded to NP x NP
+    for (int idx = threadIdx.x; idx < NP * NP; idx += kChainThreads) {
+        const int j = idx / NP, i = idx % NP;
+        Wc[j * L + i] = (j < n && i < n) ? bf.W[((int64_t)r * n + j) * ld + i] : T(0);
+    }
+    // the relation's run of tiles, its last active sample's tile and how many of
+    // that tile's pairs belong to the sample's corrupted-triple update (the tail)
+    if (w == 0) {
+        int run = 0;
+        for (int m0 = 0;; m0 += kWave) {
+            const int g = g0 + m0 + l;
+            const uint64_t b = __ballot(t0 + g < t1 && a.td_r[t0 + g] == r);
+            const int k = b == ~0ull ? kWave : __builtin_ctzll(~b);
+            run += k;
+            if (k < kWave) break;
+        }
+        const int c0 = bf.cnrows[g0] & 127;
+        const int rel = c0 > 0 && bf.cpairs[(int64_t)g0 * 2 * kCPairs + kCPairs + c0 - 1] == -2;
+        int kl = -1, gt = -1;
+        for (int g = g0 + run - 1; g >= g0 && kl < 0; --g) {
+            const int cs = a.td_cnt[t0 + g] & 255;
+            const int kk = l < cs ? a.td_kk[(t0 + g) * 8 + l] : -1;
+            const uint64_t b = __ballot(kk >= 0 && a.act[kk]);
+            if (b) {
+                kl = __shfl(kk, 63 - __builtin_clzll(b));
+                gt = g;
+            }
+        }
+        int ntail = 0;
+        if (gt >= 0) {
+            const int cp = bf.cnrows[gt] & 127;
+            const int sl = l < cp ? bf.cpairs[(int64_t)gt * 2 * kCPairs + kCPairs + l] : -3;
+            ntail = __builtin_popcountll(__ballot(sl >= 0 && (sl >> 1) == kl * 2 + 1));
+        }
+        if (l == 0) {
+            misc[3] = rel;
+            misc[4] = gt;
+            misc[5] = run;
+            misc[6] = ntail;
+        }
+    }
+    __syncthreads();
+    const int run = misc[5], has_rel = misc[3], g_tail = misc[4], n_tail = misc[6];
+    // K0 = W'^T W' (four waves, MFMA) into the P buffers, wave 0 keeps column l
+    T k0c[4 * KS];
+    {
+        T* K0 = Pbuf;
+        if (mine) {
+#pragma unroll
+            for (int ib = 0; ib < NB; ++ib) {
+                typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
+                T av[KS], bv[KS];
+#pragma unroll
+                for (int s = 0; s < KS; ++s) {
+                    av[s] = Wc[(4 * s + kq) * L + ib * 16 + l16];
+                    bv[s] = Wc[(4 * s + kq) * L + col];
+                }
+#pragma unroll
+                for (int s = 0; s < KS; ++s) acc = M::mma(av[s], bv[s], acc);
+#pragma unroll
+                for (int qq = 0; qq < 4; ++qq) K0[(ib * 16 + kq + 4 * qq) * L + col] = acc[qq];
+            }
+        }
+        __syncthreads();
+        if (w == 0) {
+            const int cK = l < NP ? l : 0;
+#pragma unroll
+            for (int i = 0; i < 4 * KS; ++i) k0c[i] = K0[i * L + cK];
+        }
+        __syncthreads();  // the P buffers are free again
+    }
+    bool changed = false;
+    tick(0);
+
+    // one 16 x 16 MFMA tile: rows rt of A (Ar) against Wc columns cb (gram = false)
+    // or against rows cb of B (gram = true); out[(rt 16 + d) * ldo + cb 16 + l16]
+    auto mfma_tile = [&](const T* Ar, const T* Bm, bool gram, int rt, int cb, T* out, int ldo) {
+        typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
+        T av[KS], bv[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            av[s] = Ar[(rt * 16 + l16) * L + 4 * s + kq];
+            bv[s] = gram ? Bm[(cb * 16 + l16) * L + 4 * s + kq] : Wc[(4 * s + kq) * L + cb * 16 + l16];
+        }
+#pragma unroll
+        for (int s = 0; s < KS; ++s) acc = M::mma(av[s], bv[s], acc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[(rt * 16 + kq + 4 * q) * ldo + cb * 16 + l16] = acc[q];
+    };
+    // rows of chunk [b, e) of the window: R NP / 256 elements a thread, in registers
+    constexpr int kRowsPer = R * NP / kChainThreads;
+    T rows[kRowsPer];
+    uint32_t rows_ok = 0;
+    auto load_rows = [&](int b, int e) {
+        int ent[kRowsPer];
+#pragma unroll
+        for (int q = 0; q < kRowsPer; ++q) {
+            const int f = b + (threadIdx.x + q * kChainThreads) / NP;
+            ent[q] = pe[f < kPipeList ? f : kPipeList - 1];
+        }
+        rows_ok = 0;
+#pragma unroll
+        for (int q = 0; q < kRowsPer; ++q) {
+            const int idx = threadIdx.x + q * kChainThreads;
+            const int k = idx / NP, j = idx % NP;
+            const bool ok = b + k < e && ent[q] >= 0 && j < n;
+            rows[q] = bf.ent[ok ? (uint32_t)ent[q] * (uint32_t)ld + (uint32_t)j : 0u];
+            rows_ok |= (ok ? 1u : 0u) << q;
+        }
+    };
+    auto store_rows = [&](int slot) {
+#pragma unroll
+        for (int q = 0; q < kRowsPer; ++q) {
+            const int idx = threadIdx.x + q * kChainThreads;
+            Abuf[slot * R * L + (idx / NP) * L + idx % NP] = ((rows_ok >> q) & 1) ? rows[q] : T(0);
+        }
+    };
+    // P_n -= lr C[:, vio] G over the chunk's nv violators (vlist; G: their rows of
+    // Pc) and the |p_j|^2 partials of the cn rows (qpart[0]; the other slices'
+    // partials zero), eight threads a row, NP / 8 columns each (on the VALU: the
+    // few violators of a chunk make an MFMA form latency-bound)
+    auto correct_q = [&](T* Pn, int cn, int nv, const T* Pc) {
+        constexpr int NE = NP / 8;
+        const int j = threadIdx.x >> 3, cb = (threadIdx.x & 7) * NE;
+        T sq = T(0);
+        if (j < cn) {
+            T x[NE];
+#pragma unroll
+            for (int u = 0; u < NE; ++u) x[u] = Pn[j * L + cb + u];
+            for (int k = 0; k < nv; ++k) {
+                const int v = vlist[k];
+                const T gl = -lr * Cx[j * LG + v];
+#pragma unroll
+                for (int u = 0; u < NE; ++u) x[u] = fma(gl, Pc[v * L + cb + u], x[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < NE; ++u) {
+                if (nv) Pn[j * L + cb + u] = x[u];
+                sq = fma(x[u], x[u], sq);
+            }
+        }
+        sq += __shfl_xor(sq, 1);
+        sq += __shfl_xor(sq, 2);
+        sq += __shfl_xor(sq, 4);
+        if ((threadIdx.x & 7) == 0) {
+            qpart[j] = j < cn ? sq : T(0);
+            for (int v = 1; v < NB; ++v) qpart[v * R + j] = T(0);
+        }
+    };
+    // the relation's last update renormalises W_c's rows before its own pairs'
+    // shrinks (transr/trainer.cpp:178-180); ends with a barrier
+    auto renorm = [&] {
+        if (mine && l < NP) {
+            T sq = T(0);
+            if (l < n)
+                for (int i = 0; i < 16; ++i) sq += Wc[l * L + 16 * w + i] * Wc[l * L + 16 * w + i];
+            rp[w * NP + l] = sq;
+        }
+        __syncthreads();
+        if (mine && l < n) {
+            T ss = rp[l];
+            for (int v = 1; v < NB; ++v) ss += rp[v * NP + l];
+            const T len = sqrt(ss);
+            for (int i = 0; i < 16; ++i) Wc[l * L + 16 * w + i] = Wc[l * L + 16 * w + i] / len;
+        }
+        __syncthreads();
+    };
+    // projections and Gram matrix of a chunk afresh, all four waves, then the |p|^2
+    // partials (two barriers; the chunk's rows are in LDS)
+    auto fresh = [&](const T* A, int cc, T* P, T* G) {
+        const int nrt = cc > 16 ? 2 : 1;
+        const int ntiles = nrt * NB + (nrt == 2 ? 3 : 1);
+        for (int tl = w; tl < ntiles; tl += kChainThreads / kWave) {
+            if (tl < nrt * NB) {
+                mfma_tile(A, nullptr, false, tl / NB, tl % NB, P, L);
+            } else {
+                const int gi = tl - nrt * NB;
+                mfma_tile(A, A, true, gi == 0 ? 0 : 1, gi == 2 ? 1 : 0, G, LG);
+            }
+        }
+        __syncthreads();
+        correct_q(P, cc, 0, nullptr);
+        __syncthreads();
+    };
+
+    int pc = 0;  // P / Gram buffer of the current chunk
+    for (int gw = g0; gw < g0 + run || gw == g0;) {
+        if (w == 0) {  // exclusive prefix of the window's tile pair counts (the relation pair left out)
+            const int nt = g0 + run - gw < kSeqMaxTiles ? g0 + run - gw : kSeqMaxTiles;
+            int carry = 0, fit = 0;
+            for (int m0 = 0; m0 < nt; m0 += kWave) {
+                const int g = m0 + l;
+                int c = g < nt ? (bf.cnrows[gw + g] & 127) : 0;
+                if (gw + g == g0 && has_rel) c -= 1;
+                int x = c;
+#pragma unroll
+                for (int s = 1; s < kWave; s <<= 1) {
+                    const int y = __shfl_up(x, s);
+                    if (l >= s) x += y;
+                }
+                if (g < nt) pre[g] = carry + x - c;
+                fit += __builtin_popcountll(__ballot(g < nt && carry + x <= kPipeList - 1));
+                carry += __shfl(x, kWave - 1);
+            }
+            if (l == 0) {
+                if (fit == nt) pre[nt] = carry;
+                misc[0] = fit;
+            }
+        }
+        __syncthreads();
+        const int ntile = misc[0];
+        const bool last = gw + ntile == g0 + run;
+        const int ntp = pre[ntile];
+        const int npairs = ntp + (last && has_rel ? 1 : 0);
+        const int tail_start = last && g_tail >= gw ? ntp - n_tail : npairs;
+        for (int f = threadIdx.x; f < npairs; f += kChainThreads) {
+            int e = r, sl = -2;
+            if (f < ntp) {
+                int lo = 0, hi = ntile - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (pre[mid] <= f) lo = mid;
+                    else hi = mid - 1;
+                }
+                const int32_t* cp = bf.cpairs + (int64_t)(gw + lo) * 2 * kCPairs;
+                e = cp[f - pre[lo]];
+                sl = cp[kCPairs + f - pre[lo]];
+            }
+            pe[f] = e;
+            ps[f] = sl;
+        }
+        // chunks of R pairs; the relation's last update's pairs (and (entity'[r], r)) alone
+        auto chunk_end = [&](int b) {
+            return b < tail_start ? (b + R < tail_start ? b + R : tail_start) : npairs;
+        };
+        __syncthreads();
+        if (npairs > 0) {
+            // prologue: rows of chunks 0 and 1 into A slots 0 and 1, chunk 2's in flight,
+            // chunk 0's projections afresh
+            const int e0 = chunk_end(0);
+            const int e1 = e0 < npairs ? chunk_end(e0) : e0;
+            load_rows(0, e0);
+            store_rows(0);
+            load_rows(e0, e1);
+            store_rows(1);
+            load_rows(e1, e1 < npairs ? chunk_end(e1) : e1);
+            if (tail_start == 0 && changed) renorm();  // (barriers: the row stores are then visible)
+            __syncthreads();
+            pc = 0;
+            fresh(Abuf, e0, Pbuf, Gbuf);
+        }
+        int ka = 0;  // A slot of the current chunk
+        for (int base = 0; base < npairs;) {
+            const int nbase = chunk_end(base);
+            const int cc = nbase - base;
+            const int nb2 = nbase < npairs ? chunk_end(nbase) : nbase;
+            const int cn = nb2 - nbase;  // pairs of the next chunk (0: none)
+            const T* A = Abuf + ka * R * L;
+            const T* An = Abuf + (ka == 2 ? 0 : ka + 1) * R * L;
+            T* P = Pbuf + pc * R * L;
+            T* Pn = Pbuf + (pc ^ 1) * R * L;
+            T* Gm = Gbuf + pc * R * LG;
+            T* Gn = Gbuf + (pc ^ 1) * R * LG;
+            ++n_chunks;
+            tick(1);
+            if (w == 0) {
+                // Walk: the pairs in order, each against the matrix the earlier ones left
+                // (transr/trainer.cpp:35-64 per pair).  A violator v's shrink
+                // W_c -= lr a_v^T g_v moves every later projection by -lr (a_j . a_v) g_v.
+                const int j = l & (R - 1);
+                T q = T(0);
+                if (j < cc) {
+                    q = qpart[j];
+                    for (int v = 1; v < NB; ++v) q += qpart[v * R + j];
+                }
+                uint32_t vmask = 0;
+                if (__ballot(j < cc && q > T(1)) != 0) {
+                    const int c0 = (l >> 5) * NH;
+                    T x[NH];  // row j, columns c0 .. c0 + NH - 1
+#pragma unroll
+                    for (int u = 0; u < NH; ++u) x[u] = P[j * L + c0 + u];
+                    int cursor = 0;
+                    const T eps = T(2) * lr;
+                    for (;;) {
+                        const uint64_t cand = __ballot(l < R && j < cc && j >= cursor && q > T(1));
+                        if (!cand) break;
+                        const int v = __builtin_ctzll(cand);
+                        const int c = l;  // column
+                        // the violator's current row to LDS for the column-lane layout
+                        if (j == v) {
+#pragma unroll
+                            for (int u = 0; u < NH; ++u) P[v * L + c0 + u] = x[u];
+                        }
+                        tick(4);
+                        const T pv = c < NP ? P[v * L + c] : T(0);
+                        T vv4[4] = {T(0), T(0), T(0), T(0)};
+#pragma unroll
+                        for (int t = 0; t < KS; ++t)
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) vv4[u] = fma(P[v * L + 4 * t + u], k0c[4 * t + u], vv4[u]);
+                        const T Vc = c < n ? (vv4[0] + vv4[1]) + (vv4[2] + vv4[3]) : T(0);
+                        tick(7);
+                        T s2[2] = {pv * Vc, Vc * Vc};
+                        wave_sums<T, 2>(s2);
+                        tick(8);
+                        const T pp = readlane_f(q, v);
+                        const T pV = s2[0], VV = s2[1], aa = Gm[v * LG + v];
+                        const T pvd = pV + aa * pp, vvd = VV + T(2) * aa * pV + aa * aa * pp;
+                        const T kappa = pvd / pp;
+                        const T w2t = vvd - kappa * pvd;
+                        const T w2 = w2t > T(0) ? w2t : T(0);
+                        const T rho = T(1) - eps * kappa;
+                        T S0, S1;
+                        const int m = transr_rounds_violator(pp, w2, eps, rho, S0, S1);
+                        n_rounds += (unsigned long long)m;
+                        max_m = max_m > (unsigned long long)m ? max_m : (unsigned long long)m;
+                        const T cpf = T(2) * (S0 + eps * S1 * kappa), cvf = T(2) * eps * S1;
+                        const T g = c < n ? cpf * pv - cvf * (Vc + aa * pv) : T(0);
+                        tick(9);
+                        if (c < NP) P[v * L + c] = g;  // the violator's row now holds G
+                        tick(10);
+                        const bool upd = j > v && j < cc;
+                        T qh = T(0);  // this lane's half of |p_j|^2
+                        if (upd) {
+                            const T gl = -lr * Gm[j * LG + v];
+                            T s4[4] = {T(0), T(0), T(0), T(0)};
+#pragma unroll
+                            for (int u = 0; u < NH; ++u) {
+                                x[u] = fma(gl, P[v * L + c0 + u], x[u]);
+                                s4[u & 3] = fma(x[u], x[u], s4[u & 3]);
+                            }
+                            qh = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+                        }
+                        {
+                            const T tot = pair_sum32(qh);  // lanes j and j + 32: the same bits
+                            if (upd) q = tot;
+                        }
+                        vmask |= 1u << v;
+                        cursor = v + 1;
+                        ++n_vio;
+                        tick(11);
+                    }
+                }
+                if (l < cc) {  // the chunk's pair flags; (entity'[r], r) marks the relation
+                    const int sl = ps[base + l];
+                    const bool vio = (vmask >> l) & 1;
+                    if (sl >= 0) bf.pflag[sl] = vio ? 1 : 0;
+                    else if (vio) bf.relpair_stamp[r] = bf.stamp;
+                }
+                if (l < R && ((vmask >> l) & 1u)) vlist[__builtin_popcount(vmask & ((1u << l) - 1u))] = l;
+                if (l == 0) {
+                    misc[1] = (int)vmask;
+                    misc[2] = __builtin_popcount(vmask);
+                }
+                tick(2);
+            } else if (cn > 0) {
+                // the next chunk against W_{k-1}: X = A_{k+1} W_c, its Gram matrix, and the
+                // cross Gram A_{k+1} A_k^T, 16 x 16 tiles dealt round waves 1-3
+                const int nrt = cn > 16 ? 2 : 1, crt = cc > 16 ? 2 : 1;
+                const int nx = nrt * NB, ng = nrt == 2 ? 3 : 1;
+                const int ntiles = nx + ng + nrt * crt;
+                for (int tl = w - 1; tl < ntiles; tl += kChainThreads / kWave - 1) {
+                    if (tl < nx) {
+                        mfma_tile(An, nullptr, false, tl / NB, tl % NB, Pn, L);
+                    } else if (tl < nx + ng) {
+                        const int gi = tl - nx;
+                        mfma_tile(An, An, true, gi == 0 ? 0 : 1, gi == 2 ? 1 : 0, Gn, LG);
+                    } else {
+                        const int ci = tl - nx - ng;
+                        mfma_tile(An, A, true, ci / crt, ci % crt, Cx, LG);
+                    }
+                }
+            }
+            __syncthreads();  // B1
+            tick(3);
+            const uint32_t vmask = (uint32_t)misc[1];
+            const int nv = misc[2];
+            // chunk k+2's rows into the slot chunk k - 1 left, chunk k+3's in flight
+            // (first: the wait for the rows loaded a chunk ago then covers no store)
+            const int ka2 = ka == 0 ? 2 : ka - 1;
+            if (nb2 < npairs || cn > 0) {
+                store_rows(ka2);
+                const int n3 = nb2 < npairs ? chunk_end(nb2) : nb2;
+                load_rows(n3, n3 < npairs ? chunk_end(n3) : n3);
+            }
+            tick(12);
+            if (vmask) {
+                changed = true;
+                // W_c[:, slice] -= lr sum_v A[v]^T G[v] over the chunk's violators
+                if (mine) {
+                    T wv[KS];
+#pragma unroll
+                    for (int t = 0; t < KS; ++t) wv[t] = Wc[(kq + 4 * t) * L + col];
+                    for (int k = 0; k < nv; ++k) {
+                        const int v = vlist[k];
+                        const T gl = -lr * P[v * L + col];
+#pragma unroll
+                        for (int t = 0; t < KS; ++t) wv[t] = fma(A[v * L + kq + 4 * t], gl, wv[t]);
+                    }
+#pragma unroll
+                    for (int t = 0; t < KS; ++t) Wc[(kq + 4 * t) * L + col] = wv[t];
+                }
+            }
+            tick(13);
+            const bool restart = nbase == tail_start && changed && cn > 0;  // the tail: afresh
+            if (cn > 0 && !restart) correct_q(Pn, cn, nv, P);
+            tick(14);
+            if (vmask) {  // the violators' pair records G (da = -lr W G made later), a wave each
+                for (int k = w; k < nv; k += kChainThreads / kWave) {
+                    const int v = vlist[k];
+                    const int sl = ps[base + v];
+                    T* dst = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
+                    if (l < n) dst[l] = P[v * L + l];
+                }
+            }
+            tick(15);
+            __syncthreads();  // B2
+            tick(6);
+            if (restart) {
+                renorm();
+                fresh(An, cn, Pn, Gn);
+            }
+            pc ^= 1;
+            ka = ka == 2 ? 0 : ka + 1;
+            base = nbase;
+        }
+        gw += ntile;
+        if (gw >= g0 + run) break;
+    }
+    // the relation's matrix back: each wave its column slice
+    if (mine && col < n)
+        for (int jj = 0; jj < n; ++jj) bf.W[((int64_t)r * n + jj) * ld + col] = Wc[jj * L + col];
+    if (bf.stats) {
+        if (threadIdx.x == 0) {
+            const unsigned long long cyc = (unsigned long long)(clock64() - ck0);
+            atomicAdd(&g_seq_stats[0], 1ull);
+            atomicAdd(&g_seq_stats[1], n_chunks);
+            atomicAdd(&g_seq_stats[2], n_vio);
+            atomicAdd(&g_seq_stats[3], n_rounds);
+            atomicAdd(&g_seq_stats[4], cyc);
+            atomicMax(&g_seq_stats[5], cyc);
+            atomicMax(&g_seq_stats[6], n_chunks);
+            atomicMax(&g_seq_stats[7], max_m);
+            for (int k = 0; k < 16; ++k) atomicAdd(&g_seq_stats[8 + k], ph[k]);
+            if (n_chunks >= 20) {
+                for (int k = 0; k < 16; ++k) atomicAdd(&g_seq_stats[24 + k], ph[k]);
+                atomicAdd(&g_seq_stats[40], n_chunks);
+                atomicAdd(&g_seq_stats[41], 1ull);
+                atomicAdd(&g_seq_stats[42], n_vio);
+            }
+        }
+    }
+}
+
+}  // namespace kb2e

@@ -6,11 +6,13 @@
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
+#include <string>
 #include <utility>
 
 #include "hip_util.hpp"
 #include "kernels_transr_cons.hpp"
 #include "kernels_transr_seq.hpp"
+#include "kernels_transr_pipe.hpp"
 #include "kernels_transr_wave.hpp"
 
 namespace kb2e {
@@ -54,11 +56,30 @@ const void* chain_fn(int n) {
     return chain_table((n + 3) / 4, std::make_integer_sequence<int, 16>{});
 }
 
+template <int... KS>
+const void* pipe_table(int ks, std::integer_sequence<int, KS...>) {
+    const void* tab[] = {(const void*)transr_cons_pipe_kernel<double, KS + 1>...};
+    return tab[ks - 1];
+}
+
+const void* pipe_fn(int n) {
+    if (!cons_wave_supported(n)) throw std::runtime_error("transRNorm pipelined chain kernel: n > 64");
+    return pipe_table((n + 3) / 4, std::make_integer_sequence<int, 16>{});
+}
+
+// KB2E_RPAR_CHAIN=serial: the unpipelined chain kernel (kernels_transr_seq.hpp)
+bool use_pipe() {
+    const char* e = getenv("KB2E_RPAR_CHAIN");
+    return !(e && std::string(e) == "serial");
+}
+
 }  // namespace
 
 size_t cons_seq_setup(int n) {
-    const size_t lds = chain_lds<double>(n);
-    HIPCHK(hipFuncSetAttribute(chain_fn(n), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const bool pipe = use_pipe();
+    const size_t lds = pipe ? pipe_lds<double>(n) : chain_lds<double>(n);
+    HIPCHK(hipFuncSetAttribute(pipe ? pipe_fn(n) : chain_fn(n), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
     return lds;
 }
 
@@ -66,7 +87,9 @@ void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, int grid, si
     RParArgs aa = a;
     RParBufs<double> bb = bf;
     void* args[] = {&aa, &bb};
-    HIPCHK(hipLaunchKernel(chain_fn(a.n), dim3(grid), dim3(kChainThreads), args, lds, stream));
+    // (the LDS size was chosen by cons_seq_setup under the same switch)
+    HIPCHK(hipLaunchKernel(lds == pipe_lds<double>(a.n) && use_pipe() ? pipe_fn(a.n) : chain_fn(a.n), dim3(grid),
+                           dim3(kChainThreads), args, lds, stream));
     const int da_grid = (int)std::min<int64_t>(2048, ((int64_t)4 * a.B + a.nr + 3) / 4);
     HIPCHK(hipLaunchKernel((const void*)transr_cons_da_kernel<double>, dim3(da_grid), dim3(256), args, 0, stream));
 }

@@ -346,7 +346,9 @@ def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
     beta lr ((hs - ts) x + sum_x (h - t)) and one unit norm; then every
     (r', w'), (h', w'), (t', w') pair of an active update with w'.a > 0.1 (the
     relation row once per sample) runs the reference's normOrth
-    (common/utils.cpp:79-111), samples in order.
+    (common/utils.cpp:79-111): first the pairs whose row only their relation
+    touches (per relation, samples in order), then the entity rows flagged
+    under several relations (samples in order).
     """
     from oracle import orc
 
@@ -395,14 +397,29 @@ def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
         _norm_rows(rel, rr)
         _norm_rows(W, rr, ignore_short=False)
         flags = []
+        ent_rels = {}  # flagged entity row -> the relations it is flagged under this batch
         for kk in a:
             rows = [(rel, r[kk]), (ent, h[kk]), (ent, t[kk]), None, (ent, nh[kk]), (ent, nt[kk])]
-            flags.append([q for q in range(6) if rows[q] is not None and W[r[kk]] @ rows[q][0][rows[q][1]] > 0.1])
-        for kk, fl in zip(a, flags):
-            rows = [(rel, r[kk]), (ent, h[kk]), (ent, t[kk]), None, (ent, nh[kk]), (ent, nt[kk])]
+            fl = [q for q in range(6) if rows[q] is not None and W[r[kk]] @ rows[q][0][rows[q][1]] > 0.1]
+            flags.append(fl)
             for q in fl:
-                tab, row = rows[q]
-                va, vb = orc.norm_orth(tab[row], W[r[kk]], rate)
-                tab[row] = va
-                W[r[kk]] = vb
+                if q != 0:
+                    ent_rels.setdefault(int(rows[q][1]), set()).add(int(r[kk]))
+        # normOrth in two passes (kernels_transh_parallel.hpp): first, per relation
+        # (samples in order), the pairs whose row no other relation touches -- the
+        # relation row and the entity rows flagged under this relation only (the
+        # relations' passes touch disjoint rows and normals, so sample order across
+        # relations is one valid order of them); then, samples in order, the
+        # entity rows flagged under several relations
+        for phase in (0, 1):
+            for kk, fl in zip(a, flags):
+                rows = [(rel, r[kk]), (ent, h[kk]), (ent, t[kk]), None, (ent, nh[kk]), (ent, nt[kk])]
+                for q in fl:
+                    shared = q != 0 and len(ent_rels[int(rows[q][1])]) > 1
+                    if shared != (phase == 1):
+                        continue
+                    tab, row = rows[q]
+                    va, vb = orc.norm_orth(tab[row], W[r[kk]], rate)
+                    tab[row] = va
+                    W[r[kk]] = vb
     return loss, active
