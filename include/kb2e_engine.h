@@ -183,7 +183,9 @@ kb2e_status kb2e_take_stats(kb2e_ctx* ctx, double* loss, int64_t* active);
  * printed at :249-250).  Energies are bit-identical FP64 restatements of the
  * reference's; ties with the true triple are not counted above it.  TransR
  * uses the zeroed (fixed) work vectors here; kb2e_evaluate_transr_compat is
- * the reference evalTransR's stateful energy.  dim <= 600. */
+ * the reference evalTransR's stateful energy.  Every dim a context takes
+ * (kb2e_create: <= 512); the ranking itself has no limit (the query rows of a
+ * rank tile are staged in LDS up to dim 600, read from L2 above). */
 kb2e_status kb2e_evaluate(kb2e_ctx* ctx, const int32_t* heads, const int32_t* tails, const int32_t* relations,
                           int64_t ntest, const int32_t* filter_heads, const int32_t* filter_tails,
                           const int32_t* filter_relations, int64_t nfilter, double* out);

@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 #include <stdexcept>
 #include <vector>
@@ -88,7 +89,7 @@ struct ProjArgs {
 template <typename T>
 __global__ __launch_bounds__(256) void eval_project_kernel(ProjArgs<T> a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < a.n) a.relv[i] = (double)a.rel[(int64_t)a.r * a.ld + i];
+    for (int k = i; k < a.n; k += (int)(gridDim.x * blockDim.x)) a.relv[k] = (double)a.rel[(int64_t)a.r * a.ld + k];
     if (i >= a.ne) return;
     const T* e = a.ent + (int64_t)i * a.ld;
     if (a.model == 0) {
@@ -135,7 +136,11 @@ __global__ __launch_bounds__(256) void eval_target_kernel(RankArgs a) {
 }
 
 // grid.x: entity blocks of 256; grid.y: query tiles of kQ.  Dynamic LDS:
-// P(true head), P(true tail) of the tile's queries [kQ][n] each + r [n].
+// P(true head), P(true tail) of the tile's queries [kQ][n] each + r [n]; when
+// that does not fit (n > 600, kRowsInLds false) the query rows are read from the
+// projection table itself (every thread of a block the same address: L1/L2
+// broadcasts), so any --size ranks, as in the reference.
+template <bool kRowsInLds>
 __global__ __launch_bounds__(256) void eval_rank_kernel(RankArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* th = lds;
@@ -144,14 +149,22 @@ __global__ __launch_bounds__(256) void eval_rank_kernel(RankArgs a) {
     __shared__ unsigned int cnt[kQ][4];
     const int q0 = blockIdx.y * kQ;
     const int nq = min(kQ, a.nq - q0);
-    for (int x = threadIdx.x; x < kQ * a.n; x += blockDim.x) {
-        const int q = x / a.n, k = x % a.n;
-        if (q < nq) {
-            th[x] = a.PT[(int64_t)k * a.ne + a.qh[q0 + q]];
-            tt[x] = a.PT[(int64_t)k * a.ne + a.qt[q0 + q]];
+    if constexpr (kRowsInLds) {
+        for (int x = threadIdx.x; x < kQ * a.n; x += blockDim.x) {
+            const int q = x / a.n, k = x % a.n;
+            if (q < nq) {
+                th[x] = a.PT[(int64_t)k * a.ne + a.qh[q0 + q]];
+                tt[x] = a.PT[(int64_t)k * a.ne + a.qt[q0 + q]];
+            }
         }
+        for (int k = threadIdx.x; k < a.n; k += blockDim.x) rv[k] = a.relv[k];
     }
-    for (int k = threadIdx.x; k < a.n; k += blockDim.x) rv[k] = a.relv[k];
+    int qhv[kQ], qtv[kQ];  // the tile's query entities (kRowsInLds false)
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+        qhv[q] = q < nq ? a.qh[q0 + q] : 0;
+        qtv[q] = q < nq ? a.qt[q0 + q] : 0;
+    }
     if (threadIdx.x < kQ * 4) cnt[threadIdx.x / 4][threadIdx.x % 4] = 0;
     __syncthreads();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -160,12 +173,15 @@ __global__ __launch_bounds__(256) void eval_rank_kernel(RankArgs a) {
 #pragma unroll
         for (int q = 0; q < kQ; ++q) eh[q] = et[q] = 0;
         for (int k = 0; k < a.n; ++k) {
-            const double v = a.PT[(int64_t)k * a.ne + i];
-            const double r = rv[k];
+            const double* col = a.PT + (int64_t)k * a.ne;
+            const double v = col[i];
+            const double r = kRowsInLds ? rv[k] : a.relv[k];
 #pragma unroll
             for (int q = 0; q < kQ; ++q) {
-                const double dh = tt[q * a.n + k] - v - r;  // (P(t) - P(i)) - r
-                const double dt = v - th[q * a.n + k] - r;  // (P(i) - P(h)) - r
+                const double pt = kRowsInLds ? tt[q * a.n + k] : col[qtv[q]];
+                const double ph = kRowsInLds ? th[q * a.n + k] : col[qhv[q]];
+                const double dh = pt - v - r;  // (P(t) - P(i)) - r
+                const double dt = v - ph - r;  // (P(i) - P(h)) - r
                 eh[q] += a.l1 ? fabs(dh) : dh * dh;
                 et[q] += a.l1 ? fabs(dt) : dt * dt;
             }
@@ -511,8 +527,10 @@ void run_chain(const EvalTables& t, CompatChainArgs<T> a) {
 void evaluate_fixed(const EvalTables& t, const EvalQuery& q, double out[4]) {
     if (q.ntest < 1) throw std::invalid_argument("empty test set");
     const int ne = t.ne, n = t.n;
-    const size_t rank_lds = (size_t)(2 * kQ + 1) * n * 8;
-    if (rank_lds > kLdsMax) throw std::invalid_argument("evaluation supports dim <= 600");
+    // n <= 600; KB2E_EVAL_ROWS_L2=1 forces the L2 form (tests)
+    const char* l2 = getenv("KB2E_EVAL_ROWS_L2");
+    const bool rows_lds = (size_t)(2 * kQ + 1) * n * 8 <= kLdsMax && !(l2 && l2[0] == '1');
+    const size_t rank_lds = rows_lds ? (size_t)(2 * kQ + 1) * n * 8 : 0;
     Grouped g = group_tests(t, q);
     DeviceFilter df;
     build_filter(t, q, df);
@@ -535,7 +553,7 @@ void evaluate_fixed(const EvalTables& t, const EvalQuery& q, double out[4]) {
     d_target.alloc(qh.size() * 8);
     d_PT.alloc((size_t)n * ne * 8);
     d_relv.alloc((size_t)n * 8);
-    allow_lds(eval_rank_kernel, rank_lds);
+    if (rows_lds) allow_lds(eval_rank_kernel<true>, rank_lds);
     for (int r = 0; r < t.nr; ++r) {
         const int64_t nq = qoff[r + 1] - qoff[r];
         if (nq == 0) continue;
@@ -557,7 +575,8 @@ void evaluate_fixed(const EvalTables& t, const EvalQuery& q, double out[4]) {
         eval_target_kernel<<<(int)((nq + 255) / 256), 256, 0, t.stream>>>(ra);
         HIPCHK(hipGetLastError());
         dim3 grid((ne + 255) / 256, (unsigned)((nq + kQ - 1) / kQ));
-        eval_rank_kernel<<<grid, 256, rank_lds, t.stream>>>(ra);
+        if (rows_lds) eval_rank_kernel<true><<<grid, 256, rank_lds, t.stream>>>(ra);
+        else eval_rank_kernel<false><<<grid, 256, 0, t.stream>>>(ra);
         HIPCHK(hipGetLastError());
     }
     std::vector<unsigned long long> counts(qh.size() * 4);

@@ -606,9 +606,16 @@ __global__ __launch_bounds__(256) void transr_cons_da_kernel(RParArgs a, RParBuf
         const T gi = l < n ? row[l] : T(0);
         const T* W = bf.W + (int64_t)r * n * ld;
         T da = T(0);
-        for (int j = 0; j < n; ++j) {
-            const T s = wave_sum(l < n ? W[(int64_t)j * ld + l] * gi : T(0));
-            if (l == j) da = s;
+        // eight rows of W at a time: their loads in flight together and eight
+        // interleaved wave reductions instead of one dependent chain a row
+        for (int j0 = 0; j0 < n; j0 += 8) {
+            T v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = (l < n && j0 + k < n) ? W[(int64_t)(j0 + k) * ld + l] * gi : T(0);
+            wave_sums<T, 8>(v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (l == j0 + k) da = v[k];
         }
         if (l < n) row[l] = -(T)a.lr * da;
     }

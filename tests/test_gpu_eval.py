@@ -161,9 +161,13 @@ def test_eval_transr_compat_without_cache():
     _compat_vs_oracle(ds, n, ent, rel, w)
 
 
-@pytest.mark.parametrize("model,dim", [("E", 200), ("H", 160)])
-def test_eval_wide_rows_matches_oracle(model, dim):
-    """dim > 128 (the reference accepts any --size)."""
+@pytest.mark.parametrize("model,dim,rows_l2", [("E", 200, "0"), ("H", 160, "0"), ("E", 512, "0"), ("E", 200, "1"),
+                                               ("H", 512, "1")])
+def test_eval_wide_rows_matches_oracle(model, dim, rows_l2, monkeypatch):
+    """dim > 128 (the reference accepts any --size; a context takes <= 512);
+    rows_l2: the rank tiles read the query rows from L2 instead of LDS (the
+    form that lifts the ranking's dim limit past 600)."""
+    monkeypatch.setenv("KB2E_EVAL_ROWS_L2", rows_l2)
     ds = tiny()
     rng = np.random.default_rng(dim)
     ent = rng.standard_normal((ds.num_entities, dim)) * 0.1

@@ -12,6 +12,9 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$ROOT"
+(while sleep 45; do date >> "$OUT/heartbeat"; done) &
+HB=$!
+trap "kill $HB" EXIT
 timeout -k 10 400 python3 bench.py --schedule "$SCHED" "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed $?"; exit 1; }
 cat "$OUT/bench.json"
 PASS="--schedule $SCHED --only --no-cpu-baseline --no-epoch --steps 100 --warmup 100"
