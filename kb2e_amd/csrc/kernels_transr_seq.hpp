@@ -589,21 +589,30 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
 template <typename T>
 __global__ __launch_bounds__(256) void transr_cons_da_kernel(RParArgs a, RParBufs<T> bf) {
     const int n = a.n, ld = a.ld, l = lane_id();
-    const int nwaves = (int)(gridDim.x * blockDim.x) >> 6;
     const int nrec = 4 * a.B + a.nr;
-    for (int q = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); q < nrec; q += nwaves) {
+    // one wave a record (grid: every record), so a record's dependent loads are
+    // the kernel's whole latency
+    {
+        const int q = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+        if (q >= nrec) return;
+        // the validity flags, the sample id and the G row are independent loads:
+        // issued together, then the relation, then its matrix rows
         int r;
         T* row;
+        bool ok;
         if (q < 4 * a.B) {
-            if (!a.act[q >> 2] || !bf.pflag[q]) continue;
-            r = a.rels[a.si[q >> 2]];
+            const uint8_t ac = a.act[q >> 2], pf = bf.pflag[q];
+            const int i0 = a.si[q >> 2];
             row = bf.pair + (int64_t)q * ld;
+            ok = ac && pf;
+            r = ok ? a.rels[i0] : 0;
         } else {
             r = q - 4 * a.B;
-            if (bf.relpair_stamp[r] != bf.stamp) continue;
             row = bf.relpair + (int64_t)r * ld;
+            ok = bf.relpair_stamp[r] == bf.stamp;
         }
-        const T gi = l < n ? row[l] : T(0);
+        const T gi = l < n ? row[l] : T(0);  // (a row of the buffer even when unused)
+        if (!ok) return;
         const T* W = bf.W + (int64_t)r * n * ld;
         T da = T(0);
         // eight rows of W at a time: their loads in flight together and eight

@@ -90,7 +90,7 @@ void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, int grid, si
     // (the LDS size was chosen by cons_seq_setup under the same switch)
     HIPCHK(hipLaunchKernel(lds == pipe_lds<double>(a.n) && use_pipe() ? pipe_fn(a.n) : chain_fn(a.n), dim3(grid),
                            dim3(kChainThreads), args, lds, stream));
-    const int da_grid = (int)std::min<int64_t>(2048, ((int64_t)4 * a.B + a.nr + 3) / 4);
+    const int da_grid = (int)(((int64_t)4 * a.B + a.nr + 3) / 4);  // a wave a record
     HIPCHK(hipLaunchKernel((const void*)transr_cons_da_kernel<double>, dim3(da_grid), dim3(256), args, 0, stream));
 }
 
