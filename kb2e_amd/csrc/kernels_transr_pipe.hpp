@@ -266,6 +266,9 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
         __syncthreads();
     };
 
+    // pairs a window: the LDS lists, or fewer (bf.chain_list >= 64 > a tile's
+    // pairs, so every window takes at least one tile)
+    const int list_cap = bf.chain_list >= 64 && bf.chain_list < kPipeList ? bf.chain_list : kPipeList;
     int pc = 0;  // P / Gram buffer of the current chunk
     for (int gw = g0; gw < g0 + run || gw == g0;) {
         if (w == 0) {  // exclusive prefix of the window's tile pair counts (the relation pair left out)
@@ -282,7 +285,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                     if (l >= s) x += y;
                 }
                 if (g < nt) pre[g] = carry + x - c;
-                fit += __builtin_popcountll(__ballot(g < nt && carry + x <= kPipeList - 1));
+                fit += __builtin_popcountll(__ballot(g < nt && carry + x <= list_cap - 1));
                 carry += __shfl(x, kWave - 1);
             }
             if (l == 0) {

@@ -154,6 +154,16 @@ def test_transr_parallel_chain_widths(dim, St, compat, monkeypatch):
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=compat)
 
 
+@pytest.mark.parametrize("dim,compat", [(50, True), (33, False)])
+def test_transr_parallel_chain_windows(dim, compat, monkeypatch):
+    """The pipelined chain kernel over several windows of a relation's pairs
+    (KB2E_RPAR_CHAIN_LIST=64 against ~90 pairs a relation a batch on the tiny
+    set; FB15k's hottest relation fits one 1,536-pair window): W_c, K0 and the
+    tail bookkeeping carry across windows, the result is the same model's."""
+    monkeypatch.setenv("KB2E_RPAR_CHAIN_LIST", "64")
+    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=8, compat=compat)
+
+
 @pytest.mark.parametrize("dim,St", [(20, 8), (50, 8)])
 def test_transr_parallel_jacobi_wave_kernel(dim, St, monkeypatch):
     """KB2E_RPAR_CONS=jacobi: the register-resident tile kernel (every pair of
