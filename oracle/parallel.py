@@ -336,6 +336,31 @@ def transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St=None, dedupe=True, 
     W[ra] += dWc[ra]
 
 
+def transh_orth_order(samples, flags, ids, r):
+    """The order of the PARALLEL TransH normOrth replays (kernels_transh_parallel.hpp
+    transh_orth_rel_kernel, then transh_orth_fix_kernel): first the (sample, row)
+    pairs whose row only their own relation touches this batch -- the relation
+    row (q = 0) and the entity rows flagged under that relation alone -- samples
+    in order (the relations' passes touch disjoint rows and normals, so this is
+    one valid order of the per-relation passes); then, samples in order, the
+    entity rows flagged under several relations.  flags[i]: the flagged row
+    slots q of samples[i] (0 relation, 1 h, 2 t, 4 h', 5 t'); ids[kk][q]: the
+    row id.  Returns [(sample, q)]."""
+    ent_rels = {}
+    for kk, fl in zip(samples, flags):
+        for q in fl:
+            if q != 0:
+                ent_rels.setdefault(int(ids[kk][q]), set()).add(int(r[kk]))
+    out = []
+    for phase in (0, 1):
+        for kk, fl in zip(samples, flags):
+            for q in fl:
+                shared = q != 0 and len(ent_rels[int(ids[kk][q])]) > 1
+                if shared == (phase == 1):
+                    out.append((kk, q))
+    return out
+
+
 def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, rate, margin=1.0):
     """Train `nbatches` TransH batches of the PARALLEL schedule in place
     (kb2e_amd/csrc/kernels_transh_parallel.hpp).  Returns (loss, active).
@@ -397,29 +422,14 @@ def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
         _norm_rows(rel, rr)
         _norm_rows(W, rr, ignore_short=False)
         flags = []
-        ent_rels = {}  # flagged entity row -> the relations it is flagged under this batch
         for kk in a:
             rows = [(rel, r[kk]), (ent, h[kk]), (ent, t[kk]), None, (ent, nh[kk]), (ent, nt[kk])]
-            fl = [q for q in range(6) if rows[q] is not None and W[r[kk]] @ rows[q][0][rows[q][1]] > 0.1]
-            flags.append(fl)
-            for q in fl:
-                if q != 0:
-                    ent_rels.setdefault(int(rows[q][1]), set()).add(int(r[kk]))
-        # normOrth in two passes (kernels_transh_parallel.hpp): first, per relation
-        # (samples in order), the pairs whose row no other relation touches -- the
-        # relation row and the entity rows flagged under this relation only (the
-        # relations' passes touch disjoint rows and normals, so sample order across
-        # relations is one valid order of them); then, samples in order, the
-        # entity rows flagged under several relations
-        for phase in (0, 1):
-            for kk, fl in zip(a, flags):
-                rows = [(rel, r[kk]), (ent, h[kk]), (ent, t[kk]), None, (ent, nh[kk]), (ent, nt[kk])]
-                for q in fl:
-                    shared = q != 0 and len(ent_rels[int(rows[q][1])]) > 1
-                    if shared != (phase == 1):
-                        continue
-                    tab, row = rows[q]
-                    va, vb = orc.norm_orth(tab[row], W[r[kk]], rate)
-                    tab[row] = va
-                    W[r[kk]] = vb
+            flags.append([q for q in range(6) if rows[q] is not None and W[r[kk]] @ rows[q][0][rows[q][1]] > 0.1])
+        ids = {kk: (r[kk], h[kk], t[kk], None, nh[kk], nt[kk]) for kk in a}
+        for kk, q in transh_orth_order(list(a), flags, ids, r):
+            rows = [(rel, r[kk]), (ent, h[kk]), (ent, t[kk]), None, (ent, nh[kk]), (ent, nt[kk])]
+            tab, row = rows[q]
+            va, vb = orc.norm_orth(tab[row], W[r[kk]], rate)
+            tab[row] = va
+            W[r[kk]] = vb
     return loss, active

@@ -157,3 +157,32 @@ def test_transr_constraint_pairs_once_per_relation():
         ent, W = ent0.copy(), W0.copy()
         transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St)
         assert np.abs(ent - want_e).max() < 1e-15 and np.abs(W - want_w).max() < 1e-15
+
+
+def test_transh_orth_order_two_passes():
+    """PARALLEL TransH normOrth order (oracle/parallel.py transh_orth_order, the
+    GPU's transh_orth_rel_kernel + transh_orth_fix_kernel): every flagged pair
+    once; with one relation it is the reference's sample order; an entity row
+    flagged under two relations waits for the second pass."""
+    from oracle.parallel import transh_orth_order
+    rng = np.random.default_rng(3)
+    n_s = 200
+    r = rng.integers(0, 5, n_s)
+    h, t = rng.integers(0, 40, n_s), rng.integers(0, 40, n_s)
+    nh, nt = rng.integers(0, 40, n_s), rng.integers(0, 40, n_s)
+    ids = {k: (r[k], h[k], t[k], None, nh[k], nt[k]) for k in range(n_s)}
+    flags = [[q for q in (0, 1, 2, 4, 5) if rng.random() < 0.3] for _ in range(n_s)]
+    order = transh_orth_order(list(range(n_s)), flags, ids, r)
+    want = [(k, q) for k in range(n_s) for q in flags[k]]
+    assert sorted(order) == sorted(want) and len(order) == len(want)
+    rels = {}
+    for k in range(n_s):
+        for q in flags[k]:
+            if q:
+                rels.setdefault(int(ids[k][q]), set()).add(int(r[k]))
+    shared = [(k, q) for k, q in order if q and len(rels[int(ids[k][q])]) > 1]
+    own = [(k, q) for k, q in order if not (q and len(rels[int(ids[k][q])]) > 1)]
+    assert order == own + shared  # each pass in sample order, the shared rows last
+    assert own == sorted(own) and shared == sorted(shared)
+    r1 = np.zeros(n_s, dtype=int)  # one relation: nothing is shared, the reference's order
+    assert transh_orth_order(list(range(n_s)), flags, ids, r1) == want
