@@ -84,8 +84,48 @@ bin/binding/train%: integration/train_gpu.cpp integration/gpu_trainer.h include/
 ref:
 	$(MAKE) -C oracle ref
 
+# ASan + UBSan builds of the host code.  CPU (tests/test_sanitize.py
+# builds the same three itself): the CLI's parser and loader + the host sample
+# stream (tests/native/host_check.cpp), the text formatter / parser, the Bloom
+# prefilter.  GPU box: libkb2e_san.so, the engine with its host code instrumented
+# (-Xarch_host: the device code is not), and the CLI on it (bin/san/train*, eval*),
+# run by tools/gpu_sanitize.sh over the golden tiny set (training, the in-process
+# two-context merge, the evaluator, the text tables).
+SANFLAGS := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all
+HIPSAN := $(foreach f,-fsanitize=address -fsanitize=undefined -fno-sanitize-recover=all -fno-omit-frame-pointer,-Xarch_host $(f))
+CLANGXX := /opt/rocm/lib/llvm/bin/clang++
+SANOBJ := kb2e_amd/build/san
+
+sanitize: bin/san/host_check bin/san/textio_check bin/san/bloom_check kb2e_amd/libkb2e_san.so bin/san/kb2e
+
+bin/san/host_check: tests/native/host_check.cpp kb2e_amd/csrc/host/kb2e_cli.cpp kb2e_amd/csrc/host_data.hpp kb2e_amd/libkb2e.so
+	@mkdir -p bin/san
+	g++ $(SANFLAGS) -std=c++17 -Iinclude -o $@ tests/native/host_check.cpp -Lkb2e_amd -lkb2e -Wl,-rpath,'$$ORIGIN/../../kb2e_amd'
+
+bin/san/textio_check: tests/native/textio_check.cpp kb2e_amd/csrc/textio.hpp
+	@mkdir -p bin/san
+	g++ $(SANFLAGS) -std=c++17 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -o $@ tests/native/textio_check.cpp
+
+bin/san/bloom_check: tests/native/bloom_check.cpp kb2e_amd/csrc/host_data.hpp
+	@mkdir -p bin/san
+	g++ $(SANFLAGS) -std=c++17 -Ikb2e_amd/csrc -o $@ tests/native/bloom_check.cpp
+
+$(SANOBJ)/%.o: kb2e_amd/csrc/%.hip $(CSRC)
+	@mkdir -p $(SANOBJ)
+	$(HIPCC) $(HIPFLAGS) $(HIPSAN) -g -c -o $@ $<
+
+kb2e_amd/libkb2e_san.so: $(SANOBJ)/engine.o $(SANOBJ)/eval.o $(SANOBJ)/textio.o $(SANOBJ)/transr_cons.o
+	$(HIPCC) $(HIPFLAGS) $(HIPSAN) -shared-libasan -shared -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
+bin/san/kb2e: kb2e_amd/csrc/host/kb2e_cli.cpp include/kb2e_engine.h kb2e_amd/libkb2e_san.so
+	@mkdir -p bin/san
+	$(CLANGXX) -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all -shared-libasan \
+	    -std=c++17 -Iinclude -o $@ kb2e_amd/csrc/host/kb2e_cli.cpp -Lkb2e_amd -l:libkb2e_san.so \
+	    -Wl,-rpath,'$$ORIGIN/../../kb2e_amd' -Wl,-rpath,$$(dirname $$($(CLANGXX) -print-file-name=libclang_rt.asan-x86_64.so))
+	for b in trainTransE trainTransH trainTransR evalTransE evalTransH evalTransR; do ln -sf kb2e bin/san/$$b; done
+
 clean:
 	rm -f kb2e_amd/libkb2e.so kb2e_amd/build/*.o bin/kb2e $(BINS) $(BINDING)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle ref clean prof binding
+.PHONY: all oracle ref clean prof binding sanitize

@@ -244,13 +244,20 @@ int64_t kb2e_device_bytes(const kb2e_ctx* ctx);
  *    kb2e_merge_epoch at every epoch boundary (collective);
  *  - one process driving N devices (one host thread, SURVEY.md 8(b)
  *    "Threading"): kb2e_comm_init_group over the N contexts, then
- *    kb2e_merge_epoch_group.  Contexts that share a device (or
- *    KB2E_MERGE_LOCAL=1) merge with plain device kernels instead of RCCL, which
- *    refuses two ranks on one GPU.
+ *    kb2e_merge_epoch_group.  Contexts that all share one device (or
+ *    KB2E_MERGE_LOCAL=1, which also needs one device) merge with plain device
+ *    kernels instead of RCCL, which refuses two ranks on one GPU; a group that
+ *    mixes shared and distinct devices is KB2E_EUNSUPPORTED.
  * Initialisation broadcasts rank 0's tables to every rank, so the ranks may
  * be created with different seeds (distinct sample streams).  The contexts must
- * agree on model, dim, table sizes and precision; their tables must be loaded
- * (kb2e_init_params / kb2e_upload_params / kb2e_transr_seed) first. */
+ * agree on model, dim, table sizes and precision (kb2e_comm_init_rank checks
+ * the other ranks' over the new communicator: KB2E_EINVAL on a difference);
+ * their tables must be loaded (kb2e_init_params / kb2e_upload_params /
+ * kb2e_transr_seed) first.  A failed init leaves the context without a
+ * communicator, so it can be retried.  The N > 1 RCCL paths (several
+ * processes, or ncclCommInitAll over several devices) are built for the
+ * 8-GPU driver run and are not exercised on the one-GPU test box: the tests
+ * cover one RCCL rank and the shared-device local backend. */
 #define KB2E_COMM_ID_BYTES 128
 kb2e_status kb2e_comm_unique_id(uint8_t* id /* KB2E_COMM_ID_BYTES */);
 kb2e_status kb2e_comm_init_rank(kb2e_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* id);

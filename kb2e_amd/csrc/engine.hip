@@ -163,6 +163,8 @@ struct kb2e_ctx {
     size_t rpar_cons_lds = 0;
     bool rpar_cons_seq = false;   // transRNorm per relation, a chain of chunks (kernels_transr_seq.hpp)
     size_t rpar_seq_lds = 0;
+    bool rpar_cons_wide = false;  // the same chain for n <= 112 off the n <= 64 matrix-core path (kernels_transr_chainw.hpp)
+    size_t rpar_wide_lds = 0;
     DevBuf rpar_pflag, rpar_cons_tile, rpar_cpairs, rpar_cnrows;
     DevBuf rpar_y, rpar_wpart, rpar_rpart, rpar_tile_act, rpar_pair, rpar_relpair, rpar_relpair_stamp, rpar_tiles,
         rpar_ntiles, rpar_tile_first, rpar_rel_begin, rpar_scan;
@@ -1656,7 +1658,7 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
                     st[0], st[1], st[2]);
             fprintf(stderr, "rpar_cons cycles: setup %llu, P0+rounds %llu, records %llu, longest block %llu, blocks %llu\n",
                     st[3], st[4], st[5], st[6], st[7]);
-            if (c->rpar_cons_seq) {
+            if (c->rpar_cons_seq || c->rpar_cons_wide) {
                 unsigned long long q[64];
                 cons_seq_take_stats(q);
                 fprintf(stderr, "rpar_cons chunk kernel: relations %llu, chunks %llu (most in a relation %llu), "

@@ -496,6 +496,7 @@ int eval_main(int argc, char** argv, kb2e_model model) {
 
 }  // namespace kb2e_host
 
+#ifndef KB2E_CLI_NO_MAIN  // (tests/native/host_check.cpp includes this file for its parser and loader)
 int main(int argc, char** argv) {
     std::string prog = argv[0];
     size_t slash = prog.find_last_of('/');
@@ -510,3 +511,4 @@ int main(int argc, char** argv) {
     fprintf(stderr, "invoke as trainTransE|H|R or evalTransE|H|R (got %s)\n", prog.c_str());
     return 2;
 }
+#endif

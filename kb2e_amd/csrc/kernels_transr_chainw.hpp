@@ -1,0 +1,489 @@
+// kernels_transr_chainw.hpp -- transRNorm of the PARALLEL TransR schedule per
+// relation, pair by pair, for every width up to 112 (FP64; the n <= 64
+// matrix-core path keeps kernels_transr_seq.hpp / kernels_transr_pipe.hpp).
+// The same model as those kernels (oracle/parallel.py transr_constraint,
+// cons="chunk1"; the reference's calls are transr/trainer.cpp:185-187 on the
+// loop at :35-64): the relation's pairs (h', r), (t', r) of its active updates
+// in (sample, update, role) order, first occurrences per relation per batch,
+// each checked against the matrix the earlier violators left; per violator v
+// (|p_v|^2 > 1, p_v = a_v W_c) the rounds of the loop in closed form along p
+// and V = p K0 (K0 = W'^T W', made at the relation's first violator;
+// transr_norm_rounds) give g, and W_c -= lr a_v^T g.  The pairs of the
+// relation's last update and (entity'[r], r) come last, after W_c's rows are
+// renormalised when anything moved; pair records G become da = -lr W G with the
+// final matrix (transr_cons_da_wide_kernel); the entity pass splits pre / post
+// deltas around the unit norm (bf.last_renorm).
+//
+// Why a second kernel.  The n <= 64 kernels keep K0's column c in lane c of one
+// wave (4 KS registers) and take their pair lists from the matrix-core gradient
+// kernel.  At n = 100 (K5, BASELINE configs[4]) a column of K0 is 100 doubles,
+// W_c alone is 91 KB of LDS, and the VALU tile path has no compacted pair lists.
+// Here:
+//  * the workgroup is one relation segment of the batch's event index; it finds
+//    the relation's last active sample, then builds its pair list in windows of
+//    256 samples (a thread a sample: its four slots, first occurrences by the
+//    per-batch (relation, entity) table, a block scan for the positions); the
+//    last update's slots are held back for the tail, so the tail is exact
+//    however many windows the relation spans;
+//  * K0 lives in registers spread over all four waves: thread t < 2 NP holds
+//    rows [h NP/2, (h + 1) NP/2) of column c = t >> 1 (h = t & 1), so V = p K0 is
+//    NP/2 FMAs a thread (p broadcast from LDS) and one lane-pair DPP add;
+//  * per chunk of 16 pairs the four waves make P = A W_c and the Gram matrix
+//    A A^T on the matrix cores (v_mfma_f64_16x16x4, runtime k-steps); the walk
+//    is workgroup-wide, three barriers a violator (the p.V / V.V partial sums,
+//    g, then the later pairs' P_j -= lr (a_j . a_v) g and |p_j|^2 afresh);
+//  * the next chunk's entity rows are loaded into registers while the current
+//    chunk is walked.
+#pragma once
+
+#include "kernels_transr_seq.hpp"
+
+namespace kb2e {
+
+constexpr int kWideRows = 16;         // pairs a chunk: one MFMA row tile
+constexpr int kWideWin = 256;         // samples a window (a thread each)
+constexpr int kWidePairs = 4 * kWideWin;
+
+__host__ __device__ constexpr int wide_nb(int n) { return (n + 15) / 16; }
+
+// LDS bytes: W_c [NK][LW] | A [R][LW] | P [R][LW] | Gram [R][R + 1] | qpart [NB][R] |
+// red [4][2] ; ints: pair entities, slots [kWidePairs] | wave sums [4] | misc [8] ; vio flags [kWidePairs]
+__host__ __device__ constexpr size_t chainw_lds(int n) {
+    return sizeof(double) * ((size_t)((n + 3) / 4 * 4) * (16 * wide_nb(n) + 2) +
+                             2 * (size_t)kWideRows * (16 * wide_nb(n) + 2) + (size_t)kWideRows * (kWideRows + 1) +
+                             (size_t)wide_nb(n) * kWideRows + 8) +
+           sizeof(int) * (2 * (size_t)kWidePairs + 4 + 8) + (size_t)kWidePairs;
+}
+
+// lane l + (l ^ 1): the two halves of a column pair
+__device__ __forceinline__ double lane_pair_sum(double x) { return x + dpp_mov<0xB1>(x); }  // quad_perm [1,0,3,2]
+
+template <int NB>
+__global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a, RParBufs<double> bf) {
+    using T = double;
+    using M = Mfma16<T>;
+    constexpr int NP = 16 * NB, LW = NP + 2, R = kWideRows, LG = R + 1, KH = NP / 2;
+    const int s = a.rel_begin[a.batch] + (int)blockIdx.x;
+    if (s >= a.batch_seg[a.batch + 1]) return;
+    const int n = a.n, ld = a.ld, KS = (n + 3) / 4, NK = 4 * KS;
+    const int r = a.seg_row[s] - a.ne;
+    const int p0 = a.seg_start[s], ns = (a.seg_start[s + 1] - p0) / 2;
+    const int tid = threadIdx.x, w = tid >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
+    const int c = tid >> 1, h = tid & 1;  // K0 / V / W-update layout: column c, half h of the rows
+    const bool colt = c < NP;             // (2 NP <= 256 threads)
+    const T lr = (T)a.lr;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* Wc = (T*)smem;            // [NK][LW]
+    T* A = Wc + NK * LW;         // [R][LW] the chunk's entity rows
+    T* P = A + R * LW;           // [R][LW] projections; the violators' rows then hold G
+    T* Gm = P + R * LW;          // [R][LG]
+    T* qpart = Gm + R * LG;      // [NB][R]
+    T* red = qpart + NB * R;     // [4][2]
+    int* pe = (int*)(red + 8);   // [kWidePairs]
+    int* ps = pe + kWidePairs;   // [kWidePairs]
+    int* wsum = ps + kWidePairs; // [4]
+    int* misc = wsum + 4;        // [8]
+    uint8_t* vflag = (uint8_t*)(misc + 8);  // [kWidePairs]
+    const long long ck0 = clock64();
+    unsigned long long n_chunks = 0, n_vio = 0, n_rounds = 0, max_m = 0;
+
+    // the relation's last active sample (from the end, 256 samples a round)
+    if (tid == 0) misc[0] = -1;
+    __syncthreads();
+    for (int qb = ns - kWideWin;; qb -= kWideWin) {
+        const int q = qb + tid;
+        const bool act = q >= 0 && q < ns && a.act[a.kl.kk_of(a.keys[p0 + 2 * q])];
+        const uint64_t b = __ballot(act);
+        if (b && l == 0) atomicMax(&misc[0], qb + (w << 6) + 63 - __builtin_clzll(b));
+        __syncthreads();
+        const int found = misc[0];
+        __syncthreads();  // (read by every thread before the next round's atomics)
+        if (found >= 0 || qb <= 0) break;
+    }
+    const int klq = misc[0];
+    if (klq < 0) return;  // no active update: the gradient step left the relation alone
+    const int kl = a.kl.kk_of(a.keys[p0 + 2 * klq]);
+    const bool has_rel = r < a.ne && ptab_first(a, r, r) < 0;  // (entity'[r], r), transr/trainer.cpp:187
+
+    // W'_r, zero padded to NK x NP
+    for (int idx = tid; idx < NK * NP; idx += 256) {
+        const int j = idx / NP, i = idx % NP;
+        Wc[j * LW + i] = (j < n && i < n) ? bf.W[((int64_t)r * n + j) * ld + i] : T(0);
+    }
+    T k0[KH];
+#pragma unroll
+    for (int i = 0; i < KH; ++i) k0[i] = T(0);
+    bool have_k0 = false, changed = false;
+
+    // the chunk's rows: R x NP elements, NB a thread, into registers (every load is
+    // issued, padding zeroed when stored: no register written under a branch while a
+    // load into it is in flight)
+    T rows[NB];
+    uint32_t rows_ok = 0;
+    auto load_rows = [&](int b, int e) {
+        int ent[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const int f = b + (tid + q * 256) / NP;
+            ent[q] = f < e ? pe[f] : -1;
+        }
+        rows_ok = 0;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const int j = (tid + q * 256) % NP;
+            const bool ok = ent[q] >= 0 && j < n;
+            rows[q] = bf.ent[ok ? (uint32_t)ent[q] * (uint32_t)ld + (uint32_t)j : 0u];
+            rows_ok |= (ok ? 1u : 0u) << q;
+        }
+    };
+    auto store_rows = [&]() {
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const int idx = tid + q * 256;
+            A[(idx / NP) * LW + idx % NP] = ((rows_ok >> q) & 1) ? rows[q] : T(0);
+        }
+    };
+
+    // One chunk: pairs [b, b + cc) of the LDS list, rows already in `rows`; the rows of
+    // [nb, ne) are loaded while it is walked.  Leaves W_c updated and vflag set.
+    auto chunk = [&](int b, int cc, int nb, int ne) {
+        ++n_chunks;
+        store_rows();
+        __syncthreads();  // A (and W_c) ready
+        if (nb < ne) load_rows(nb, ne);
+        // P = A W_c (NB column tiles) and the Gram tile, dealt round the waves
+        for (int tl = w; tl <= NB; tl += 4) {
+            const bool gram = tl == NB;
+            typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
+            for (int kb = 0; kb < KS; kb += 8) {
+                T av[8], bv[8];
+#pragma unroll
+                for (int s8 = 0; s8 < 8; ++s8) {
+                    const int k = 4 * (kb + s8) + kq;
+                    const bool ok = kb + s8 < KS;
+                    av[s8] = ok ? A[l16 * LW + k] : T(0);
+                    bv[s8] = ok ? (gram ? A[l16 * LW + k] : Wc[k * LW + tl * 16 + l16]) : T(0);
+                }
+#pragma unroll
+                for (int s8 = 0; s8 < 8; ++s8)
+                    if (kb + s8 < KS) acc = M::mma(av[s8], bv[s8], acc);
+            }
+            if (gram) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) Gm[(kq + 4 * q) * LG + l16] = acc[q];
+            } else {
+                T sp[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    P[(kq + 4 * q) * LW + tl * 16 + l16] = acc[q];
+                    sp[q] = acc[q] * acc[q];
+                }
+                row16_sums<T, 4>(sp);
+                if (l16 == 0) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) qpart[tl * R + kq + 4 * q] = sp[q];
+                }
+            }
+        }
+        __syncthreads();  // P, Gram, |p|^2 partials
+        const int j = l16;  // |p_j|^2 of pair j in lanes j, j + 16, ... of every wave
+        T qj = T(0);
+        if (j < cc) {
+            qj = qpart[j];
+            for (int v = 1; v < NB; ++v) qj += qpart[v * R + j];
+        }
+        uint32_t cand = (uint32_t)__ballot(l < R && j < cc && qj > T(1));
+        if (!cand) return;
+        if (!have_k0) {  // K0[:, c] rows of half h = sum_j W[j][i] W[j][c] (W_c is still W'_r)
+            have_k0 = true;
+            if (colt) {
+                for (int jr = 0; jr < n; ++jr) {
+                    const T wc = Wc[jr * LW + c];
+                    const double2* wrow = (const double2*)(Wc + jr * LW + h * KH);
+#pragma unroll
+                    for (int i2 = 0; i2 < KH / 2; ++i2) {
+                        const double2 x = wrow[i2];
+                        k0[2 * i2] = fma(x.x, wc, k0[2 * i2]);
+                        k0[2 * i2 + 1] = fma(x.y, wc, k0[2 * i2 + 1]);
+                    }
+                }
+            }
+        }
+        const T eps = T(2) * lr;
+        uint32_t vmask = 0;
+        for (int cursor = 0;;) {
+            cand &= ~((1u << cursor) - 1);
+            if (!cand) break;
+            const int v = __builtin_ctz(cand);
+            // V_c = sum_i p_v[i] K0[i][c], the two halves of the rows in lanes 2c, 2c + 1
+            T V = T(0), pv = T(0);
+            if (colt) {
+                T acc4[4] = {T(0), T(0), T(0), T(0)};
+                const double2* prow = (const double2*)(P + v * LW + h * KH);
+#pragma unroll
+                for (int i2 = 0; i2 < KH / 2; ++i2) {
+                    const double2 x = prow[i2];
+                    acc4[(2 * i2) & 3] = fma(x.x, k0[2 * i2], acc4[(2 * i2) & 3]);
+                    acc4[(2 * i2 + 1) & 3] = fma(x.y, k0[2 * i2 + 1], acc4[(2 * i2 + 1) & 3]);
+                }
+                V = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
+                pv = P[v * LW + c];
+            }
+            V = lane_pair_sum(V);
+            T s2[2] = {colt && h == 0 ? pv * V : T(0), colt && h == 0 ? V * V : T(0)};
+            wave_sums<T, 2>(s2);
+            if (l == 0) {
+                red[2 * w] = s2[0];
+                red[2 * w + 1] = s2[1];
+            }
+            __syncthreads();  // (1) the partial sums
+            const T pV = (red[0] + red[2]) + (red[4] + red[6]);
+            const T VV = (red[1] + red[3]) + (red[5] + red[7]);
+            const T pp = readlane_f(qj, v);
+            const T aa = Gm[v * LG + v];  // |a_v|^2
+            const T pvd = pV + aa * pp, vvd = VV + T(2) * aa * pV + aa * aa * pp;
+            const T kappa = pvd / pp;
+            const T w2t = vvd - kappa * pvd;
+            const T w2 = w2t > T(0) ? w2t : T(0);
+            const T rho = T(1) - eps * kappa;
+            T S0, S1;
+            const int m = transr_rounds_violator(pp, w2, eps, rho, S0, S1);
+            n_rounds += (unsigned long long)m;
+            max_m = max_m > (unsigned long long)m ? max_m : (unsigned long long)m;
+            const T cpf = T(2) * (S0 + eps * S1 * kappa), cvf = T(2) * eps * S1;
+            if (colt && h == 0) P[v * LW + c] = c < n ? cpf * pv - cvf * (V + aa * pv) : T(0);
+            __syncthreads();  // (2) g in P's row v
+            {  // the later pairs: P[jr] -= lr (a_jr . a_v) g, |p_jr|^2 afresh (16 lanes a row)
+                const int jr = tid >> 4, s16 = tid & 15;
+                const bool later = jr > v && jr < cc;
+                if (later) {
+                    const T gl = -lr * Gm[jr * LG + v];
+                    T sq = T(0);
+#pragma unroll
+                    for (int k = 0; k < NB; ++k) {
+                        const int ci = s16 + 16 * k;
+                        const T x = fma(gl, P[v * LW + ci], P[jr * LW + ci]);
+                        P[jr * LW + ci] = x;
+                        sq = fma(x, x, sq);
+                    }
+                    T sv[1] = {sq};
+                    row16_sums<T, 1>(sv);
+                    if (s16 == 0) qpart[jr] = sv[0];  // (qpart row 0 is free once read)
+                }
+            }
+            __syncthreads();  // (3) the new |p_j|^2
+            if (j > v && j < cc) qj = qpart[j];
+            cand = (uint32_t)__ballot(l < R && j < cc && j > v && qj > T(1));
+            vmask |= 1u << v;
+            cursor = v + 1;
+            ++n_vio;
+        }
+        // the violators' records G, flags, and W_c[k][c] -= lr sum_v a_v[k] G_v[c]
+        changed = true;
+        for (uint32_t mm = vmask; mm; mm &= mm - 1) {
+            const int v = __builtin_ctz(mm);
+            const int sl = ps[b + v];
+            if (colt && h == 0 && c < n) {
+                T* dst = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
+                dst[c] = P[v * LW + c];
+            }
+            if (tid == 0) {
+                vflag[b + v] = 1;
+                if (sl < 0) bf.relpair_stamp[r] = bf.stamp;
+            }
+        }
+        if (colt && c < n) {  // (rows of half h of column c: this thread's alone)
+            const int k1 = min(n, (h + 1) * KH);
+            for (uint32_t mm = vmask; mm; mm &= mm - 1) {
+                const int v = __builtin_ctz(mm);
+                const T gl = -lr * P[v * LW + c];
+                for (int k = h * KH; k < k1; ++k) Wc[k * LW + c] = fma(A[v * LW + k], gl, Wc[k * LW + c]);
+            }
+        }
+    };
+
+    // windows of 256 samples up to the last active one; the last update's slots wait for the tail
+    for (int wq = 0; wq <= klq; wq += kWideWin) {
+        const int q = wq + tid;
+        int kk = -1, ents[4] = {-1, -1, -1, -1};
+        uint32_t keep = 0;
+        if (q <= klq) {
+            kk = a.kl.kk_of(a.keys[p0 + 2 * q]);
+            if (a.act[kk]) {
+                const int i0 = a.si[kk], jj = a.sj[kk];
+                const int hh = a.heads[i0], tt = a.tails[i0];
+                const bool sd = a.side[kk] != 0;
+                ents[0] = hh;
+                ents[1] = tt;
+                ents[2] = sd ? hh : jj;
+                ents[3] = sd ? jj : tt;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int sl = kk * 4 + k;
+                    const bool tail = kk == kl && k >= 2;
+                    if (!tail && ptab_first(a, r, ents[k]) == sl) keep |= 1u << k;
+                }
+            } else {
+                kk = -1;
+            }
+        }
+        const int cnt = __builtin_popcount(keep);
+        int x = cnt;
+#pragma unroll
+        for (int sh = 1; sh < kWave; sh <<= 1) {
+            const int y = __shfl_up(x, sh);
+            if (l >= sh) x += y;
+        }
+        if (l == kWave - 1) wsum[w] = x;
+        __syncthreads();
+        int off = 0;
+        for (int k = 0; k < w; ++k) off += wsum[k];
+        const int npw = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+        const int pos0 = off + x - cnt;
+        {
+            int pos = pos0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((keep >> k) & 1) {
+                    pe[pos] = ents[k];
+                    ps[pos] = kk * 4 + k;
+                    vflag[pos] = 0;
+                    ++pos;
+                }
+        }
+        __syncthreads();  // the window's list
+        if (npw > 0) {
+            load_rows(0, min(R, npw));
+            for (int b = 0; b < npw; b += R) {
+                const int e = min(b + R, npw);
+                chunk(b, e - b, e, min(e + R, npw));
+                __syncthreads();  // W_c, and A / P free for the next chunk
+            }
+        }
+        // the flags of the window's slots (the tail's wait)
+        if (kk >= 0) {
+            int pos = pos0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (kk == kl && k >= 2) continue;
+                uint8_t f = 0;
+                if ((keep >> k) & 1) f = vflag[pos++];
+                bf.pflag[kk * 4 + k] = f;
+            }
+        }
+        __syncthreads();  // the list is rebuilt by the next window
+    }
+
+    // the tail: the last update's pairs and (entity'[r], r), after the rows' renorm
+    int ntail = 0;
+    uint32_t tkeep = 0;
+    {
+        const int i0 = a.si[kl], jj = a.sj[kl];
+        const int hh = a.heads[i0], tt = a.tails[i0];
+        const bool sd = a.side[kl] != 0;
+        const int e2[2] = {sd ? hh : jj, sd ? jj : tt};
+        for (int k = 0; k < 2; ++k)
+            if (ptab_first(a, r, e2[k]) == kl * 4 + 2 + k) {
+                tkeep |= 1u << k;
+                if (tid == 0) {
+                    pe[ntail] = e2[k];
+                    ps[ntail] = kl * 4 + 2 + k;
+                    vflag[ntail] = 0;
+                }
+                ++ntail;
+            }
+        if (has_rel) {
+            if (tid == 0) {
+                pe[ntail] = r;
+                ps[ntail] = -2;
+                vflag[ntail] = 0;
+            }
+            ++ntail;
+        }
+    }
+    if (ntail > 0) {
+        if (changed) {  // the last update's unit rows (transr/trainer.cpp:178-180)
+            const int jr = c;
+            T sq = T(0);
+            if (colt && jr < n)
+                for (int i = h * KH; i < min(n, (h + 1) * KH); ++i) sq = fma(Wc[jr * LW + i], Wc[jr * LW + i], sq);
+            const T len = sqrt(lane_pair_sum(sq));
+            __syncthreads();
+            if (colt && jr < n)
+                for (int i = h * KH; i < min(n, (h + 1) * KH); ++i) Wc[jr * LW + i] = Wc[jr * LW + i] / len;
+        }
+        __syncthreads();  // the tail list and W_c
+        load_rows(0, ntail);
+        chunk(0, ntail, ntail, ntail);
+        __syncthreads();
+    }
+    if (tid == 0) {
+        int pos = 0;
+        for (int k = 0; k < 2; ++k) bf.pflag[kl * 4 + 2 + k] = ((tkeep >> k) & 1) ? vflag[pos++] : 0;
+    }
+    // the relation's matrix back
+    for (int idx = tid; idx < n * n; idx += 256) {
+        const int j = idx / n, i = idx % n;
+        bf.W[((int64_t)r * n + j) * ld + i] = Wc[j * LW + i];
+    }
+    if (bf.stats && tid == 0) {
+        const unsigned long long cyc = (unsigned long long)(clock64() - ck0);
+        atomicAdd(&g_seq_stats[0], 1ull);
+        atomicAdd(&g_seq_stats[1], n_chunks);
+        atomicAdd(&g_seq_stats[2], n_vio);
+        atomicAdd(&g_seq_stats[3], n_rounds);
+        atomicAdd(&g_seq_stats[4], cyc);
+        atomicMax(&g_seq_stats[5], cyc);
+        atomicMax(&g_seq_stats[6], n_chunks);
+        atomicMax(&g_seq_stats[7], max_m);
+    }
+}
+
+// The pair records for n <= 128: transr_cons_da_kernel with two elements a lane
+// (G_i, i = 2l, 2l + 1; da_j = sum_i W[j][i] G_i by interleaved wave sums).
+static __attribute__((unused)) __global__ __launch_bounds__(256) void transr_cons_da_wide_kernel(RParArgs a,
+                                                                                                 RParBufs<double> bf) {
+    using T = double;
+    const int n = a.n, ld = a.ld, l = lane_id();
+    const int nrec = 4 * a.B + a.nr;
+    const int q = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (q >= nrec) return;
+    int r;
+    T* row;
+    bool ok;
+    if (q < 4 * a.B) {
+        const uint8_t ac = a.act[q >> 2], pf = bf.pflag[q];
+        const int i0 = a.si[q >> 2];
+        row = bf.pair + (int64_t)q * ld;
+        ok = ac && pf;
+        r = ok ? a.rels[i0] : 0;
+    } else {
+        r = q - 4 * a.B;
+        row = bf.relpair + (int64_t)r * ld;
+        ok = bf.relpair_stamp[r] == bf.stamp;
+    }
+    T g[2];
+    lane_pair_load(row, n, g);
+    if (!ok) return;
+    const T* W = bf.W + (int64_t)r * n * ld;
+    T da[2] = {T(0), T(0)};
+    for (int j0 = 0; j0 < n; j0 += 8) {
+        T v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            T wr[2] = {T(0), T(0)};
+            if (j0 + k < n) lane_pair_load(W + (int64_t)(j0 + k) * ld, n, wr);
+            v[k] = wr[0] * g[0] + wr[1] * g[1];
+        }
+        wave_sums<T, 8>(v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (2 * l == j0 + k) da[0] = v[k];
+            if (2 * l + 1 == j0 + k) da[1] = v[k];
+        }
+    }
+    const T out[2] = {-(T)a.lr * da[0], -(T)a.lr * da[1]};
+    lane_pair_store(row, n, out);
+}
+
+}  // namespace kb2e

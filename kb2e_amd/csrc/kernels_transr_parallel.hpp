@@ -175,6 +175,7 @@ struct RParBufs {
     int32_t last_renorm; // transRNorm pass: entity rows renormalised between pre / post pair deltas (kernels_transr_seq.hpp)
     int32_t dbg;         // transRNorm wave kernel: phases skipped for timing experiments (tools; wrong results)
     int32_t chain_list;  // pipelined chain kernel: pairs a window (0: all that fit the LDS; tests force windows)
+    int32_t chain_tiles; // chain kernels: tiles a window (0: the prefix table's 256; tests force windows)
 };
 
 __host__ __device__ constexpr int rm_up16_host_dev(int v) { return (v + 15) & ~15; }

@@ -268,11 +268,14 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
 
     // pairs a window: the LDS lists, or fewer (bf.chain_list >= 64 > a tile's
     // pairs, so every window takes at least one tile)
+    // tiles a window: the prefix table, or fewer (bf.chain_tiles >= 1: tests force
+    // windows that end before the relation's trailing inactive tiles)
+    const int tile_cap = bf.chain_tiles >= 1 && bf.chain_tiles < kSeqMaxTiles ? bf.chain_tiles : kSeqMaxTiles;
     const int list_cap = bf.chain_list >= 64 && bf.chain_list < kPipeList ? bf.chain_list : kPipeList;
     int pc = 0;  // P / Gram buffer of the current chunk
     for (int gw = g0; gw < g0 + run || gw == g0;) {
         if (w == 0) {  // exclusive prefix of the window's tile pair counts (the relation pair left out)
-            const int nt = g0 + run - gw < kSeqMaxTiles ? g0 + run - gw : kSeqMaxTiles;
+            const int nt = g0 + run - gw < tile_cap ? g0 + run - gw : tile_cap;
             int carry = 0, fit = 0;
             for (int m0 = 0; m0 < nt; m0 += kWave) {
                 const int g = m0 + l;
@@ -295,7 +298,10 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
         }
         __syncthreads();
         const int ntile = misc[0];
-        const bool last = gw + ntile == g0 + run;
+        // the window holding the relation's last active sample is its last: the
+        // tiles after it hold no pairs (only inactive samples), so a window cut by
+        // the tile cap after it would otherwise lose the tail's renorm
+        const bool last = gw + ntile == g0 + run || (g_tail >= 0 && gw + ntile > g_tail);
         const int ntp = pre[ntile];
         const int npairs = ntp + (last && has_rel ? 1 : 0);
         const int tail_start = last && g_tail >= gw ? ntp - n_tail : npairs;
@@ -511,7 +517,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
             base = nbase;
         }
         gw += ntile;
-        if (gw >= g0 + run) break;
+        if (last || gw >= g0 + run) break;
     }
     // the relation's matrix back: each wave its column slice
     if (mine && col < n)

@@ -227,11 +227,12 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
     T k0c[4 * KS];  // wave 0: K0's column l (the violators' V rows), loaded once K0 is made
     tick(0);
     int chunk_no = 0;  // chunks so far (row buffer parity)
+    const int tile_cap = bf.chain_tiles >= 1 && bf.chain_tiles < kSeqMaxTiles ? bf.chain_tiles : kSeqMaxTiles;
     // windows of at most kSeqMaxTiles tiles and kChainList - 1 pairs (FB15k's hottest
     // relation holds ~1000 pairs a batch: one window)
     for (int gw = g0; gw < g0 + run || gw == g0;) {
         if (w == 0) {  // exclusive prefix of the window's tile pair counts (the relation pair left out)
-            const int nt = g0 + run - gw < kSeqMaxTiles ? g0 + run - gw : kSeqMaxTiles;
+            const int nt = g0 + run - gw < tile_cap ? g0 + run - gw : tile_cap;
             int carry = 0, fit = 0;
             for (int m0 = 0; m0 < nt; m0 += kWave) {
                 const int g = m0 + l;
@@ -255,7 +256,10 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
         }
         __syncthreads();
         const int ntile = misc[0];
-        const bool last = gw + ntile == g0 + run;
+        // the window holding the relation's last active sample is its last: the
+        // tiles after it hold no pairs (only inactive samples), so a window cut by
+        // the tile cap after it would otherwise lose the tail's renorm
+        const bool last = gw + ntile == g0 + run || (g_tail >= 0 && gw + ntile > g_tail);
         const int ntp = pre[ntile];
         const int npairs = ntp + (last && has_rel ? 1 : 0);
         const int tail_start = last && g_tail >= gw ? ntp - n_tail : npairs;
@@ -553,7 +557,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
             base = nbase;
         }
         gw += ntile;
-        if (gw >= g0 + run) break;
+        if (last || gw >= g0 + run) break;
     }
     // the relation's matrix back: each wave its column slice (the transRNorm pass adds no partials)
     if (mine && col < n)

@@ -12,6 +12,7 @@
 #include "hip_util.hpp"
 #include "kernels_transr_cons.hpp"
 #include "kernels_transr_seq.hpp"
+#include "kernels_transr_chainw.hpp"
 #include "kernels_transr_pipe.hpp"
 #include "kernels_transr_wave.hpp"
 
@@ -67,6 +68,19 @@ const void* pipe_fn(int n) {
     return pipe_table((n + 3) / 4, std::make_integer_sequence<int, 16>{});
 }
 
+const void* chainw_fn(int n) {
+    switch (wide_nb(n)) {
+        case 1: return (const void*)transr_cons_chain_wide_kernel<1>;
+        case 2: return (const void*)transr_cons_chain_wide_kernel<2>;
+        case 3: return (const void*)transr_cons_chain_wide_kernel<3>;
+        case 4: return (const void*)transr_cons_chain_wide_kernel<4>;
+        case 5: return (const void*)transr_cons_chain_wide_kernel<5>;
+        case 6: return (const void*)transr_cons_chain_wide_kernel<6>;
+        case 7: return (const void*)transr_cons_chain_wide_kernel<7>;
+    }
+    throw std::runtime_error("transRNorm wide chain kernel: n > 112");
+}
+
 // KB2E_RPAR_CHAIN=serial: the unpipelined chain kernel (kernels_transr_seq.hpp)
 bool use_pipe() {
     const char* e = getenv("KB2E_RPAR_CHAIN");
@@ -92,6 +106,25 @@ void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, int grid, si
                            dim3(kChainThreads), args, lds, stream));
     const int da_grid = (int)(((int64_t)4 * a.B + a.nr + 3) / 4);  // a wave a record
     HIPCHK(hipLaunchKernel((const void*)transr_cons_da_kernel<double>, dim3(da_grid), dim3(256), args, 0, stream));
+}
+
+bool cons_chainw_supported(int n) { return n >= 1 && n <= kWideMaxN; }
+
+size_t cons_chainw_setup(int n) {
+    const size_t lds = chainw_lds(n);
+    HIPCHK(hipFuncSetAttribute(chainw_fn(n), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    return lds;
+}
+
+void cons_chainw_launch(const RParArgs& a, const RParBufs<double>& bf, size_t lds, hipStream_t stream) {
+    RParArgs aa = a;
+    RParBufs<double> bb = bf;
+    void* args[] = {&aa, &bb};
+    // one workgroup per relation segment of the batch (at most min(|R|, B) of them)
+    const int grid = std::min(a.nr, a.B);
+    HIPCHK(hipLaunchKernel(chainw_fn(a.n), dim3(grid), dim3(256), args, lds, stream));
+    const int da_grid = (int)(((int64_t)4 * a.B + a.nr + 3) / 4);  // a wave a record
+    HIPCHK(hipLaunchKernel((const void*)transr_cons_da_wide_kernel, dim3(da_grid), dim3(256), args, 0, stream));
 }
 
 bool cons_wave_supported(int n) { return n >= 1 && n <= 64; }

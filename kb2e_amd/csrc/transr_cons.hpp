@@ -9,6 +9,7 @@
 
 namespace kb2e {
 
+constexpr int kWideMaxN = 112;  // the wide chain's W_c [n][NP + 2] + chunk buffers fit the 160 KB LDS
 constexpr int kConsPpt = 1;  // transRNorm matrix partials per tile (transr_rel_rows_kernel cons_ppt)
 
 // Does the kernel cover this width (n <= 64)?
@@ -32,6 +33,13 @@ void grad_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, hipStr
 // the pair records' kernel after it.
 size_t cons_seq_setup(int n);
 void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, int grid, size_t lds, hipStream_t stream);
+// transRNorm per relation, pair by pair, for n <= 112 (kernels_transr_chainw.hpp; FP64,
+// any path: the VALU tile kernels at n = 100): is the width covered, its dynamic LDS
+// (the limit raised to it), and the launch of the chain (one workgroup per relation
+// segment of the batch) and of its pair records' kernel.
+bool cons_chainw_supported(int n);
+size_t cons_chainw_setup(int n);
+void cons_chainw_launch(const RParArgs& a, const RParBufs<double>& bf, size_t lds, hipStream_t stream);
 // The chunk kernel's counters (relations, chunks, violators, rounds, cycles sum / max,
 // most chunks of a relation), reset.
 void cons_seq_take_stats(unsigned long long (&st)[64]);

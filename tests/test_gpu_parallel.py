@@ -84,13 +84,14 @@ def test_transe_parallel_deterministic():
 
 def _cons_form(dim, mfma):
     """The transRNorm form the engine runs (engine_transr_parallel.inc): the
-    per-relation sequential kernel (every pair against the matrix the earlier
-    ones left) on the matrix-core path for n <= 64, unless KB2E_RPAR_CONS picks
-    the Jacobi tile / wave kernels."""
+    per-relation sequential chain (every pair against the matrix the earlier
+    ones left) in FP64 up to n = 112 -- kernels_transr_seq.hpp / _pipe.hpp on
+    the n <= 64 matrix-core path, kernels_transr_chainw.hpp elsewhere -- unless
+    KB2E_RPAR_CONS picks the Jacobi tile / wave kernels; Jacobi above 112."""
     ck = os.environ.get("KB2E_RPAR_CONS", "")
-    if mfma and dim <= 64 and ck not in ("tile", "jacobi"):
-        return "chunk1"
-    return "jacobi"
+    if ck in ("tile", "jacobi") or dim > 112:
+        return "jacobi"
+    return "chunk1"
 
 
 def _transr_vs_model(ds, dim, epochs, monkeypatch, *, St=8, compat=False, distance=0, batches=10, rate=0.01,
@@ -128,7 +129,8 @@ def _transr_vs_model(ds, dim, epochs, monkeypatch, *, St=8, compat=False, distan
 
 @pytest.mark.parametrize("mfma", [True, False])
 @pytest.mark.parametrize("dim,distance,St", [(20, 0, 8), (20, 1, 4), (50, 0, 8), (33, 0, 2), (40, 0, 8), (64, 0, 1),
-                                             (65, 0, 2), (96, 0, 8), (100, 0, 8), (100, 1, 4), (128, 0, 1)])
+                                             (65, 0, 2), (96, 0, 8), (100, 0, 8), (100, 1, 4), (112, 0, 2),
+                                             (128, 0, 1)])
 def test_transr_parallel_fixed(dim, distance, St, mfma, monkeypatch):
     """Fixed (zeroed) energy; tiles of St samples (several per hot relation); the
     matrix-core kernels and the VALU ones.  St must not exceed the engine's own
@@ -154,14 +156,37 @@ def test_transr_parallel_chain_widths(dim, St, compat, monkeypatch):
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=compat)
 
 
-@pytest.mark.parametrize("dim,compat", [(50, True), (33, False)])
-def test_transr_parallel_chain_windows(dim, compat, monkeypatch):
-    """The pipelined chain kernel over several windows of a relation's pairs
+@pytest.mark.parametrize("chain", ["pipe", "serial"])
+@pytest.mark.parametrize("dim,compat,env,St", [(50, True, "KB2E_RPAR_CHAIN_LIST=64", 8),
+                                               (33, False, "KB2E_RPAR_CHAIN_LIST=64", 8),
+                                               (50, True, "KB2E_RPAR_CHAIN_TILES=2", 1),
+                                               (20, False, "KB2E_RPAR_CHAIN_TILES=3", 1)])
+def test_transr_parallel_chain_windows(dim, compat, env, St, chain, monkeypatch):
+    """The chain kernels over several windows of a relation's pairs
     (KB2E_RPAR_CHAIN_LIST=64 against ~90 pairs a relation a batch on the tiny
     set; FB15k's hottest relation fits one 1,536-pair window): W_c, K0 and the
-    tail bookkeeping carry across windows, the result is the same model's."""
-    monkeypatch.setenv("KB2E_RPAR_CHAIN_LIST", "64")
-    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=8, compat=compat)
+    tail bookkeeping carry across windows, the result is the same model's.
+    KB2E_RPAR_CHAIN_TILES caps the tiles a window (one sample a tile), so the
+    window holding the relation's last active sample usually ends before the
+    relation's trailing inactive tiles: the tail (the last update's pairs after
+    W_c's rows are renormalised) must still be isolated there."""
+    name, val = env.split("=")
+    monkeypatch.setenv(name, val)
+    if chain == "serial":
+        monkeypatch.setenv("KB2E_RPAR_CHAIN", "serial")
+    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=compat)
+
+
+@pytest.mark.parametrize("dim,compat,mfma", [(100, True, False), (100, False, False), (72, True, True),
+                                             (20, True, False)])
+def test_transr_parallel_wide_chain_windows(dim, compat, mfma, monkeypatch):
+    """The wide chain kernel (kernels_transr_chainw.hpp) over several 256-sample
+    windows of a relation: the small set's hottest relation holds ~700 samples
+    a batch (B = 3,000), so W_c, K0 and the held-back tail (the relation's last
+    update) carry across windows; n = 20 on the VALU path runs it at one column
+    tile."""
+    _transr_vs_model(data.synthetic("small", seed=1), dim, 1, monkeypatch, St=2 if mfma else 8, compat=compat,
+                     mfma=mfma, rate=0.001)
 
 
 @pytest.mark.parametrize("dim,St", [(20, 8), (50, 8)])
