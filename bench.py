@@ -354,13 +354,18 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
     else:
         dominant, avg_ms, bytes_per_launch = "score", score_ms / max(1, score_n), score_b * B
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = None
+    # HBM bytes per launch from the PMC counters (FETCH_SIZE + WRITE_SIZE): counter
+    # passes cannot share this timed run (separate rocprofv3 --pmc runs,
+    # tools/gpu_profile.sh), so the value is read from the committed profile of the
+    # same command, named in traffic_source
+    traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}_{schedule}_f{args.precision}.json")
     if os.path.exists(pmc):
         try:
             fams = json.load(open(pmc))
             v = fams.get(dominant, {}).get("hbm_bytes_per_launch")
             traffic = float(v) if v else None
+            traffic_src = os.path.relpath(pmc, ROOT) if traffic else None
         except (OSError, ValueError):
             traffic = None
     epoch_rec = None
@@ -388,7 +393,8 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
         "late_epoch": late_rec,
         "active_fraction": a,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "kernel": dominant,
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": dominant,
                      "kernel_avg_us": avg_ms * 1e3, "algorithmic_bytes_per_launch": bytes_per_launch,
                      "kernels_avg_us": kernels_us, "step_achieved_GBs": per_sample * samples / elapsed / 1e9},
     }

@@ -202,7 +202,7 @@ kb2e_status kb2e_evaluate(kb2e_ctx* ctx, const int32_t* heads, const int32_t* ta
  * triple's (std::sort orders those arbitrarily, :138; they are ranked after
  * the truth here).  `progress` (may be NULL) is called after each relation
  * with the fraction of test triples done (the reference prints it, :240).
- * dim <= 140. */
+ * Every dim a context takes (W in LDS up to 140, read from L2 above). */
 kb2e_status kb2e_evaluate_transr_compat(kb2e_ctx* ctx, const int32_t* heads, const int32_t* tails,
                                         const int32_t* relations, int64_t ntest, const int32_t* filter_heads,
                                         const int32_t* filter_tails, const int32_t* filter_relations,

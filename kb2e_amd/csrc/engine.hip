@@ -84,6 +84,7 @@ struct kb2e_ctx {
     std::string err;
     GlibcRand rng{1};
     TripleStore ts;
+    DevBuf rel_order;  // relation ids by training frequency, most frequent first
     bool have_triples = false, have_params = false;
     int tables_read = 0;  // kb2e_read_table: bit t = table t loaded from text
     int n = 0, ld = 0, ch = 1, nw = 2, esize = 8;
@@ -1301,6 +1302,15 @@ kb2e_status kb2e_upload_triples(kb2e_ctx* c, const int32_t* h, const int32_t* t,
         c->filter_bloom.alloc(c->ts.filter.bloom.size() * 8);
         HIPCHK(hipMemcpy(c->filter_bloom.p, c->ts.filter.bloom.data(), c->ts.filter.bloom.size() * 8,
                          hipMemcpyHostToDevice));
+        {  // relations by training frequency, most frequent first (the PARALLEL TransR chain
+           // kernels start the hot relations' long chains first: kernels_transr_chainw.hpp)
+            std::vector<int32_t> order((size_t)c->cfg.num_relations);
+            for (int32_t q = 0; q < c->cfg.num_relations; ++q) order[q] = q;
+            std::stable_sort(order.begin(), order.end(),
+                             [&](int32_t x, int32_t y) { return c->ts.rel_count[x] > c->ts.rel_count[y]; });
+            c->rel_order.alloc(order.size() * 4);
+            HIPCHK(hipMemcpy(c->rel_order.p, order.data(), order.size() * 4, hipMemcpyHostToDevice));
+        }
         std::vector<double> pr(c->ts.pr);
         if (c->cfg.method == 0) std::fill(pr.begin(), pr.end(), 500.0);  // common/trainer.cpp:84-86
         c->pr_dev.alloc(pr.size() * 8);
@@ -1664,8 +1674,13 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
                 fprintf(stderr, "rpar_cons chunk kernel: relations %llu, chunks %llu (most in a relation %llu), "
                         "violators %llu, rounds %llu (most %llu), cycles mean %.0f max %llu\n", q[0], q[1], q[6], q[2],
                         q[3], q[7], q[0] ? (double)q[4] / (double)q[0] : 0.0, q[5]);
-                fprintf(stderr, "rpar_cons chunk phases (prologue, issue+renorm, P+Gram+B1, K0, violators, B2, "
-                        "W update+rows+B3; violator: V, sums, rounds, record, update):");
+                if (c->rpar_cons_wide)
+                    fprintf(stderr, "rpar_cons wide chain phases (prologue, window list, rows+barrier, P+Gram+B1, "
+                            "K0, V+sums, B(1), rounds+g, B(2), later pairs, B(3), records+W update, chunk barrier, "
+                            "window flags, tail, write-back):");
+                else
+                    fprintf(stderr, "rpar_cons chunk phases (prologue, issue+renorm, P+Gram+B1, K0, violators, B2, "
+                            "W update+rows+B3; violator: V, sums, rounds, record, update):");
                 for (int k = 8; k < 24; ++k) fprintf(stderr, " %llu", q[k]);
                 fprintf(stderr, "; hot relations (%llu, %llu chunks, %llu violators):", q[41], q[40], q[42]);
                 for (int k = 24; k < 40; ++k) fprintf(stderr, " %llu", q[k]);

@@ -226,6 +226,7 @@ struct CompatChainArgs {
     const T* rel;
     const T* W;  // [nr][n][ld]
     int32_t n, ld, ne, l1, G;
+    int32_t wglob;  // W read from global memory (L2) instead of an LDS image: dims whose n x n image does not fit
     const CompatPass* passes;
     int32_t npass;
     const int32_t* ftime;
@@ -236,8 +237,8 @@ struct CompatChainArgs {
 
 constexpr int kChainThreads = 192;  // wave 0: chain, wave 1: energies, wave 2: loader
 
-__host__ __device__ constexpr size_t chain_lds_bytes(int n, int G) {
-    return 8 * ((size_t)n * n + 3 * (size_t)G * n + 3 * (size_t)n) + 4 * (3 * (size_t)G + 8);
+__host__ __device__ constexpr size_t chain_lds_bytes(int n, int G, bool wglob = false) {
+    return 8 * ((wglob ? 0 : (size_t)n * n) + 3 * (size_t)G * n + 3 * (size_t)n) + 4 * (3 * (size_t)G + 8);
 }
 
 // The calls of `npass` passes in the reference's order.  Each step: the loader
@@ -252,8 +253,8 @@ template <typename T, int CH>
 __global__ __launch_bounds__(kChainThreads) void compat_chain_kernel(CompatChainArgs<T> a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int n = a.n, G = a.G;
-    double* Wl = lds;                        // [n][n]: W[j][i] of the current relation
-    double* slots = Wl + (size_t)n * n;      // [3][G][n]: candidate rows, then the call's terms
+    double* Wl = lds;                        // [n][n]: W[j][i] of the current relation (LDS image)
+    double* slots = Wl + (a.wglob ? 0 : (size_t)n * n);  // [3][G][n]: candidate rows, then the call's terms
     double* bvec = slots + (size_t)3 * G * n;  // [3][n]: the pass's fixed entity row
     int* ids = (int*)(bvec + 3 * n);         // [3][G]
     int* cnt = ids + 3 * G;                  // [3]
@@ -325,7 +326,8 @@ __global__ __launch_bounds__(kChainThreads) void compat_chain_kernel(CompatChain
                 if (ps.rel != cur_rel) {
                     cur_rel = ps.rel;
                     const T* Wg = a.W + (int64_t)cur_rel * n * a.ld;
-                    for (int idx = l; idx < n * n; idx += 64) Wl[idx] = (double)Wg[(int64_t)(idx / n) * a.ld + idx % n];
+                    if (!a.wglob)
+                        for (int idx = l; idx < n * n; idx += 64) Wl[idx] = (double)Wg[(int64_t)(idx / n) * a.ld + idx % n];
 #pragma unroll
                     for (int c = 0; c < CH; ++c) {
                         const int i = l + 64 * c;
@@ -341,6 +343,7 @@ __global__ __launch_bounds__(kChainThreads) void compat_chain_kernel(CompatChain
                     va[c] = ps.side == 0 ? hv[c] : tv[c];
                     fa[c] = ps.side == 0 ? tv[c] : hv[c];
                 }
+                const T* Wg = a.W + (int64_t)cur_rel * n * a.ld;  // (the wglob form: rows of ld, from L2)
                 for (int q = 0; q < k; ++q) {
                     double* x = slots + ((size_t)C * G + q) * n;
 #pragma unroll
@@ -348,10 +351,18 @@ __global__ __launch_bounds__(kChainThreads) void compat_chain_kernel(CompatChain
                         const int i = l + 64 * c;
                         if (i < n) {
                             double v = va[c], f = fa[c];
-                            for (int j = 0; j < n; ++j) {
-                                const double w = Wl[j * n + i];
-                                v += w * x[j];
-                                f += w * y[j];
+                            if (a.wglob) {
+                                for (int j = 0; j < n; ++j) {
+                                    const double w = (double)Wg[(int64_t)j * a.ld + i];
+                                    v += w * x[j];
+                                    f += w * y[j];
+                                }
+                            } else {
+                                for (int j = 0; j < n; ++j) {
+                                    const double w = Wl[j * n + i];
+                                    v += w * x[j];
+                                    f += w * y[j];
+                                }
                             }
                             va[c] = v;
                             fa[c] = f;
@@ -513,12 +524,17 @@ void launch_chain(const EvalTables& t, const CompatChainArgs<T>& a, size_t lds) 
 template <typename T>
 void run_chain(const EvalTables& t, CompatChainArgs<T> a) {
     if (a.npass == 0) return;
-    const size_t lds = chain_lds_bytes(t.n, a.G);
+    const size_t lds = chain_lds_bytes(t.n, a.G, a.wglob != 0);
     switch ((t.n + 63) / 64) {
         case 1: launch_chain<T, 1>(t, a, lds); break;
         case 2: launch_chain<T, 2>(t, a, lds); break;
         case 3: launch_chain<T, 3>(t, a, lds); break;
-        default: throw std::invalid_argument("TransR compat evaluation supports dim <= 140");
+        case 4: launch_chain<T, 4>(t, a, lds); break;
+        case 5: launch_chain<T, 5>(t, a, lds); break;
+        case 6: launch_chain<T, 6>(t, a, lds); break;
+        case 7: launch_chain<T, 7>(t, a, lds); break;
+        case 8: launch_chain<T, 8>(t, a, lds); break;
+        default: throw std::invalid_argument("TransR compat evaluation supports dim <= 512");
     }
 }
 
@@ -601,13 +617,20 @@ void evaluate_transr_compat(const EvalTables& t, const EvalQuery& q, double* wor
     if (t.model != 2) throw std::invalid_argument("compat evaluation is TransR's");
     if (q.ntest < 1) throw std::invalid_argument("empty test set");
     const int ne = t.ne, n = t.n;
+    // W's n x n image in LDS up to dim 140; above it the chain wave reads W from L2
+    // (every dim a context takes; KB2E_EVAL_W_L2=1 forces that form in the tests)
+    const char* wl2 = getenv("KB2E_EVAL_W_L2");
     int G = 0;
-    for (int g : {64, 32, 16, 8, 4})
-        if (chain_lds_bytes(n, g) <= kLdsMax) {
-            G = g;
-            break;
-        }
-    if (G == 0 || n > 192) throw std::invalid_argument("TransR compat evaluation supports dim <= 140");
+    bool wglob = false;
+    for (int pass = 0; pass < 2 && G == 0; ++pass) {
+        wglob = pass == 1 || (wl2 && wl2[0] == '1');
+        for (int g : {64, 32, 16, 8, 4})
+            if (chain_lds_bytes(n, g, wglob) <= kLdsMax) {
+                G = g;
+                break;
+            }
+    }
+    if (G == 0 || n > 512) throw std::invalid_argument("TransR compat evaluation supports dim <= 512");
     Grouped g = group_tests(t, q);
     DeviceFilter df;
     build_filter(t, q, df);
@@ -643,12 +666,12 @@ void evaluate_transr_compat(const EvalTables& t, const EvalQuery& q, double* wor
                               t.stream));
         if (t.f64) {
             CompatChainArgs<double> a{(const double*)t.ent, (const double*)t.rel, (const double*)t.w, n, t.ld, ne, t.l1, G,
-                                d_chain.as<CompatPass>(), (int32_t)chain.size(), d_ftime.as<int32_t>(),
+                                wglob, d_chain.as<CompatPass>(), (int32_t)chain.size(), d_ftime.as<int32_t>(),
                                 d_work.as<double>(), cache_on ? d_cache.as<double>() : nullptr, d_pbuf.as<double>()};
             run_chain<double>(t, a);
         } else {
             CompatChainArgs<float> a{(const float*)t.ent, (const float*)t.rel, (const float*)t.w, n, t.ld, ne, t.l1, G,
-                               d_chain.as<CompatPass>(), (int32_t)chain.size(), d_ftime.as<int32_t>(),
+                               wglob, d_chain.as<CompatPass>(), (int32_t)chain.size(), d_ftime.as<int32_t>(),
                                d_work.as<double>(), cache_on ? d_cache.as<double>() : nullptr, d_pbuf.as<double>()};
             run_chain<float>(t, a);
         }

@@ -63,10 +63,25 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
     using T = double;
     using M = Mfma16<T>;
     constexpr int NP = 16 * NB, LW = NP + 2, R = kWideRows, LG = R + 1, KH = NP / 2;
-    const int s = a.rel_begin[a.batch] + (int)blockIdx.x;
-    if (s >= a.batch_seg[a.batch + 1]) return;
+    // block b takes the b-th most frequent relation, so the long chains of the hot
+    // relations start first (a hot relation dispatched late would add its wait to the
+    // batch); its segment in this batch's index by binary search over the batch's
+    // relation segments (sorted by row), none: nothing to do
+    const int r = a.rel_order[blockIdx.x];
+    int s;
+    {
+        int lo = a.rel_begin[a.batch], hi = a.batch_seg[a.batch + 1] - 1;
+        if (lo > hi) return;
+        const int want = a.ne + r;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (a.seg_row[mid] < want) lo = mid + 1;
+            else hi = mid;
+        }
+        if (a.seg_row[lo] != want) return;
+        s = lo;
+    }
     const int n = a.n, ld = a.ld, KS = (n + 3) / 4, NK = 4 * KS;
-    const int r = a.seg_row[s] - a.ne;
     const int p0 = a.seg_start[s], ns = (a.seg_start[s + 1] - p0) / 2;
     const int tid = threadIdx.x, w = tid >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
     const int c = tid >> 1, h = tid & 1;  // K0 / V / W-update layout: column c, half h of the rows
@@ -86,6 +101,20 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
     uint8_t* vflag = (uint8_t*)(misc + 8);  // [kWidePairs]
     const long long ck0 = clock64();
     unsigned long long n_chunks = 0, n_vio = 0, n_rounds = 0, max_m = 0;
+    // KB2E_RPAR_STATS: cycles of the phases on thread 0 (g_seq_stats 8..23; relations of
+    // >= 200 chunks also 24..39, their chunks / count / violators 40..42): 0 prologue,
+    // 1 window list, 2 rows + A barrier, 3 P / Gram MFMA + B1, 4 |p|^2 + K0, 5 V + sums,
+    // 6 barrier (1), 7 rounds + g, 8 barrier (2), 9 later pairs, 10 barrier (3), 11 records +
+    // W update, 12 end-of-chunk barrier, 13 window flags, 14 tail, 15 write-back
+    unsigned long long ph[16] = {};
+    long long tq = ck0;
+    auto tick = [&](int k) {
+        if (bf.stats && tid == 0) {
+            const long long t = clock64();
+            ph[k] += (unsigned long long)(t - tq);
+            tq = t;
+        }
+    };
 
     // the relation's last active sample (from the end, 256 samples a round)
     if (tid == 0) misc[0] = -1;
@@ -114,6 +143,7 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
 #pragma unroll
     for (int i = 0; i < KH; ++i) k0[i] = T(0);
     bool have_k0 = false, changed = false;
+    tick(0);
 
     // the chunk's rows: R x NP elements, NB a thread, into registers (every load is
     // issued, padding zeroed when stored: no register written under a branch while a
@@ -151,6 +181,7 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
         store_rows();
         __syncthreads();  // A (and W_c) ready
         if (nb < ne) load_rows(nb, ne);
+        tick(2);
         // P = A W_c (NB column tiles) and the Gram tile, dealt round the waves
         for (int tl = w; tl <= NB; tl += 4) {
             const bool gram = tl == NB;
@@ -186,6 +217,7 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
             }
         }
         __syncthreads();  // P, Gram, |p|^2 partials
+        tick(3);
         const int j = l16;  // |p_j|^2 of pair j in lanes j, j + 16, ... of every wave
         T qj = T(0);
         if (j < cc) {
@@ -193,7 +225,10 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
             for (int v = 1; v < NB; ++v) qj += qpart[v * R + j];
         }
         uint32_t cand = (uint32_t)__ballot(l < R && j < cc && qj > T(1));
-        if (!cand) return;
+        if (!cand) {
+            tick(4);
+            return;
+        }
         if (!have_k0) {  // K0[:, c] rows of half h = sum_j W[j][i] W[j][c] (W_c is still W'_r)
             have_k0 = true;
             if (colt) {
@@ -209,6 +244,7 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
                 }
             }
         }
+        tick(4);
         const T eps = T(2) * lr;
         uint32_t vmask = 0;
         for (int cursor = 0;;) {
@@ -236,7 +272,9 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
                 red[2 * w] = s2[0];
                 red[2 * w + 1] = s2[1];
             }
+            tick(5);
             __syncthreads();  // (1) the partial sums
+            tick(6);
             const T pV = (red[0] + red[2]) + (red[4] + red[6]);
             const T VV = (red[1] + red[3]) + (red[5] + red[7]);
             const T pp = readlane_f(qj, v);
@@ -252,7 +290,9 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
             max_m = max_m > (unsigned long long)m ? max_m : (unsigned long long)m;
             const T cpf = T(2) * (S0 + eps * S1 * kappa), cvf = T(2) * eps * S1;
             if (colt && h == 0) P[v * LW + c] = c < n ? cpf * pv - cvf * (V + aa * pv) : T(0);
+            tick(7);
             __syncthreads();  // (2) g in P's row v
+            tick(8);
             {  // the later pairs: P[jr] -= lr (a_jr . a_v) g, |p_jr|^2 afresh (16 lanes a row)
                 const int jr = tid >> 4, s16 = tid & 15;
                 const bool later = jr > v && jr < cc;
@@ -271,12 +311,14 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
                     if (s16 == 0) qpart[jr] = sv[0];  // (qpart row 0 is free once read)
                 }
             }
+            tick(9);
             __syncthreads();  // (3) the new |p_j|^2
             if (j > v && j < cc) qj = qpart[j];
             cand = (uint32_t)__ballot(l < R && j < cc && j > v && qj > T(1));
             vmask |= 1u << v;
             cursor = v + 1;
             ++n_vio;
+            tick(10);
         }
         // the violators' records G, flags, and W_c[k][c] -= lr sum_v a_v[k] G_v[c]
         changed = true;
@@ -300,6 +342,7 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
                 for (int k = h * KH; k < k1; ++k) Wc[k * LW + c] = fma(A[v * LW + k], gl, Wc[k * LW + c]);
             }
         }
+        tick(11);
     };
 
     // windows of 256 samples up to the last active one; the last update's slots wait for the tail
@@ -352,12 +395,14 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
                 }
         }
         __syncthreads();  // the window's list
+        tick(1);
         if (npw > 0) {
             load_rows(0, min(R, npw));
             for (int b = 0; b < npw; b += R) {
                 const int e = min(b + R, npw);
                 chunk(b, e - b, e, min(e + R, npw));
                 __syncthreads();  // W_c, and A / P free for the next chunk
+                tick(12);
             }
         }
         // the flags of the window's slots (the tail's wait)
@@ -372,6 +417,7 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
             }
         }
         __syncthreads();  // the list is rebuilt by the next window
+        tick(13);
     }
 
     // the tail: the last update's pairs and (entity'[r], r), after the rows' renorm
@@ -421,6 +467,7 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
         int pos = 0;
         for (int k = 0; k < 2; ++k) bf.pflag[kl * 4 + 2 + k] = ((tkeep >> k) & 1) ? vflag[pos++] : 0;
     }
+    tick(14);
     // the relation's matrix back
     for (int idx = tid; idx < n * n; idx += 256) {
         const int j = idx / n, i = idx % n;
@@ -436,6 +483,14 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
         atomicMax(&g_seq_stats[5], cyc);
         atomicMax(&g_seq_stats[6], n_chunks);
         atomicMax(&g_seq_stats[7], max_m);
+        tick(15);
+        for (int k = 0; k < 16; ++k) atomicAdd(&g_seq_stats[8 + k], ph[k]);
+        if (n_chunks >= 200) {  // the hot relations alone
+            for (int k = 0; k < 16; ++k) atomicAdd(&g_seq_stats[24 + k], ph[k]);
+            atomicAdd(&g_seq_stats[40], n_chunks);
+            atomicAdd(&g_seq_stats[41], 1ull);
+            atomicAdd(&g_seq_stats[42], n_vio);
+        }
     }
 }
 

@@ -74,6 +74,7 @@ struct RParArgs {
     const int32_t* td_cnt;    // [tiles] samples | 256 when the tile is its relation's only one
     const int32_t* td_kk;     // [tiles][8] batch-local sample of tile sample q
     const int32_t* td_ent;    // [tiles][8][4] entity of row (q, h / t / h' / t'), -1 past cnt
+    const int32_t* rel_order; // [nr] relation ids, most frequent in training first (chain kernels' block order)
 };
 
 // The per-batch (relation, entity) -> first active update slot table.  A pair

@@ -120,8 +120,8 @@ void cons_chainw_launch(const RParArgs& a, const RParBufs<double>& bf, size_t ld
     RParArgs aa = a;
     RParBufs<double> bb = bf;
     void* args[] = {&aa, &bb};
-    // one workgroup per relation segment of the batch (at most min(|R|, B) of them)
-    const int grid = std::min(a.nr, a.B);
+    // one workgroup per relation, most frequent first (those absent from the batch exit)
+    const int grid = a.nr;
     HIPCHK(hipLaunchKernel(chainw_fn(a.n), dim3(grid), dim3(256), args, lds, stream));
     const int da_grid = (int)(((int64_t)4 * a.B + a.nr + 3) / 4);  // a wave a record
     HIPCHK(hipLaunchKernel((const void*)transr_cons_da_wide_kernel, dim3(da_grid), dim3(256), args, 0, stream));

@@ -141,6 +141,18 @@ def test_eval_transr_compat_tiny_dims(n, distance):
     _compat_vs_oracle(ds, n, ent, rel, w, distance=distance)
 
 
+@pytest.mark.parametrize("n,w_l2", [(200, "0"), (160, "0"), (50, "1")])
+def test_eval_transr_compat_wide(n, w_l2, monkeypatch):
+    """Above dim 140 W's n x n image no longer fits the LDS and the chain wave
+    reads it from L2 (the reference's evalTransR takes any --size,
+    transr/evaluation.cpp:22-32); KB2E_EVAL_W_L2=1 forces that form at n = 50.
+    Still bit-identical to the oracle's energies."""
+    monkeypatch.setenv("KB2E_EVAL_W_L2", w_l2)
+    ds = tiny()
+    ent, rel, w = _random_transr(ds, n, n)
+    _compat_vs_oracle(ds, n, ent, rel, w, test=ds.test[:60])
+
+
 def test_eval_transr_compat_small_set_with_state():
     """2,000 entities (the per-relation cache on), 1,000 test triples over 40
     relations, starting from non-zero work vectors (a process that already

@@ -29,6 +29,24 @@ from kb2e_amd.linkpred import train_and_evaluate, transe_seed  # noqa: E402
 METRICS = ("filtered_rank", "filtered_hits10", "raw_rank", "raw_hits10", "final_loss", "mean_loss_last10")
 
 
+# two-sided 95 % Student t quantiles by degrees of freedom
+T975 = {1: 12.706, 2: 4.303, 3: 3.182, 4: 2.776, 5: 2.571, 6: 2.447, 7: 2.365, 8: 2.306, 9: 2.262, 10: 2.228}
+
+
+def paired_interval(d):
+    """Mean of the paired deltas, its standard error and 95 % t interval."""
+    d = np.asarray(d, dtype=np.float64)
+    k = len(d)
+    mean = float(d.mean())
+    if k < 2:
+        return {"n": k, "mean": mean}
+    se = float(d.std(ddof=1) / np.sqrt(k))
+    t = T975.get(k - 1, 1.96)
+    lo, hi = mean - t * se, mean + t * se
+    return {"n": k, "mean": mean, "se": se, "ci95": [lo, hi], "covers_zero": bool(lo <= 0.0 <= hi),
+            "same_sign": int(max((d > 0).sum(), (d < 0).sum()))}
+
+
 def summarize(rows, schedules):
     out = {"seeds": [r["seed"] for r in rows]}
     for s in schedules:
@@ -49,10 +67,13 @@ def summarize(rows, schedules):
                       "rel_delta_of_means": (p[m]["mean"] - o[m]["mean"]) / abs(o[m]["mean"]),
                       "ordered_rel_spread": (o[m]["max"] - o[m]["min"]) / abs(o[m]["mean"]),
                       "parallel_mean_inside_ordered_envelope": o[m]["min"] <= p[m]["mean"] <= o[m]["max"]}
-        # paired per-seed deltas (same stream, same init)
-        for m in ("filtered_rank", "final_loss"):
-            d = [(r["parallel"][m] - r["ordered"][m]) / abs(r["ordered"][m]) for r in rows]
-            cmp[m]["paired_rel_delta"] = d
+        # paired per-seed deltas (same stream, same init) with a 95 % t interval of
+        # their mean: a systematic term shows as an interval that excludes 0 even
+        # when the schedules' means sit inside each other's cross-seed spread
+        for m in METRICS:
+            d = np.array([(r["parallel"][m] - r["ordered"][m]) / abs(r["ordered"][m]) for r in rows])
+            cmp[m]["paired_rel_delta"] = d.tolist()
+            cmp[m]["paired"] = paired_interval(d)
         Lo = np.array(o["loss_envelope"]["min"]), np.array(o["loss_envelope"]["max"])
         Lp = np.array(p["loss_envelope"]["mean"])
         cmp["parallel_mean_loss_epochs_inside_ordered_envelope"] = int(((Lp >= Lo[0]) & (Lp <= Lo[1])).sum())
@@ -73,7 +94,29 @@ def main():
     ap.add_argument("--seeds", default="7,8,9")
     ap.add_argument("--schedules", default="ordered,parallel")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--summarize", nargs="*", default=None,
+                    help="only write the summary of the per-seed rows in these JSONL files (runs split over calls)")
     args = ap.parse_args()
+    if args.summarize is not None:
+        by_seed = {}  # rows of one seed from several files (e.g. ORDERED and PARALLEL runs) merged
+        for fn in args.summarize:
+            for line in open(fn):
+                r = json.loads(line)
+                if "seed" in r and "summary" not in r:
+                    by_seed.setdefault(r["seed"], {}).update(r)
+        rows = [by_seed[k] for k in sorted(by_seed)]
+        schedules = tuple(s for s in ("ordered", "parallel") if all(s in r for r in rows))
+        r0 = rows[0]
+        ds = data.synthetic(args.shape, seed=0)
+        summ = {"summary": summarize(rows, schedules), "model": r0["model"], "dim": r0["dim"],
+                "transr_compat": r0["transr_compat"], "epochs": r0["epochs"], "shape": args.shape,
+                "random_hits10": 10.0 / ds.num_entities, "files": args.summarize}
+        with open(args.out, "a") as f:
+            for r in rows:
+                f.write(json.dumps(r) + "\n")
+            f.write(json.dumps(summ) + "\n")
+        print(json.dumps(summ["summary"].get("compare", {})))
+        return
     dim = args.dim or {"E": 100, "H": 100, "R": 50}[args.model]
     schedules = tuple(args.schedules.split(","))
     ds = data.synthetic(args.shape, seed=0)
