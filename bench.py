@@ -277,8 +277,13 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
             done += k
             run.pos += k
             if merger is not None and run.pos % batches == 0:
+                t0 = time.perf_counter()  # (the merge returns once the merged tables are in place)
                 merger.merge()
+                run.merge_s += time.perf_counter() - t0
+                run.merges += 1
     run.pos = 0
+    run.merge_s = 0.0
+    run.merges = 0
 
     def to_epoch_start():
         if run.pos % batches:
@@ -299,11 +304,14 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
     to_epoch_start()  # the timed batches start an epoch (its sampling commit + index build inside)
     eng.synchronize()
     eng.take_stats()
+    run.merge_s, run.merges = 0.0, 0  # merges inside the timed batches only
     # HIP-event timing of the batch kernels on every 10th batch (events cost
     # device time; sampling keeps the timed run unperturbed); per-epoch kernels always
     eng.profile(10)
     elapsed = timed(steps)
+    merge_s, merges = run.merge_s, run.merges
     loss, active = eng.take_stats()
+    device_bytes = eng.device_bytes()
     # phase B span: TransE/TransH "fold_phase" (ordered: per-row folds; parallel:
     # the apply kernels), TransR "apply" (parallel) or the relation owners (ordered)
     if model == "R":
@@ -338,13 +346,15 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
     if dist is not None:
         import torch
 
-        t = torch.tensor([elapsed, float(samples), float(active)], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, float(samples), float(active), merge_s, float(merges), float(device_bytes)],
+                         dtype=torch.float64, device="cuda")
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed = float(mx[0])
         samples = float(t[1])
         active = float(t[2])
+        merge_s, merges, device_bytes = float(mx[3]), int(mx[4]), int(mx[5])
     a = active / max(1.0, samples)
     s = 8 if args.precision == 64 else 4
     score_b, fold_b = phase_bytes(model, dim, s, a)
@@ -387,8 +397,13 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
             late_s = float(t[0])
         late_rec = {"value": batches * B * world / late_s, "ms": late_s * 1e3, "batches": batches,
                     "epoch_index": late}
+    merge_rec = None
+    if merger is not None:  # the epoch merge's share of the timed region (max over ranks)
+        merge_rec = {"merges": merges, "ms_per_merge": merge_s / merges * 1e3 if merges else None,
+                     "share_of_timed": merge_s / elapsed, "kind": type(merger).__name__}
     return {
         "value": samples / elapsed, "ms_per_step": elapsed / steps * 1e3, "B": B, "batches": batches,
+        "merge": merge_rec, "device_bytes_per_gpu": device_bytes,
         "epoch": epoch_rec,
         "late_epoch": late_rec,
         "active_fraction": a,
@@ -475,8 +490,12 @@ def main():
                    "schedule": args.schedule},
         "roofline": main_run["roofline"],
         "active_fraction": main_run["active_fraction"],
-        "timing": "K batches from an epoch boundary (epoch sampling commit + index build inside)",
+        "timing": "K batches from an epoch boundary (epoch sampling commit + index build inside"
+                  + (", the epoch merges falling inside them" if world > 1 else "") + ")",
+        "device_bytes_per_gpu": main_run["device_bytes_per_gpu"],
     }
+    if main_run["merge"] is not None:
+        out["merge"] = main_run["merge"]
     out["schedules"] = {args.schedule: {"value": main_run["value"], "ms_per_step": main_run["ms_per_step"],
                                         "epoch": main_run["epoch"], "late_epoch": main_run["late_epoch"]}}
     if other_run is not None:

@@ -95,7 +95,10 @@ const char* kb2e_last_error(const kb2e_ctx* ctx);
 /* Trainer::add for every training triple, in train-file order, plus the
  * per-relation head/tail co-occurrence means of Trainer::loadFiles
  * (common/trainer.cpp:26-32, 151-201).  Builds the negative-sample filter and
- * the Bernoulli table on the device. */
+ * the Bernoulli table on the device.  Contexts take dim <= 512 for evaluation
+ * and the table calls; training has narrower limits, checked here:
+ * KB2E_EUNSUPPORTED for ORDERED TransR above dim 138 (FP64) / 195 (FP32), the
+ * relation owner's matrix in LDS (PARALLEL TransR: dim <= 128 at kb2e_create). */
 kb2e_status kb2e_upload_triples(kb2e_ctx* ctx, const int32_t* heads, const int32_t* tails,
                                 const int32_t* relations, int64_t count);
 

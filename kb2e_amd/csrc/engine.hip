@@ -164,6 +164,7 @@ struct kb2e_ctx {
     size_t rpar_cons_lds = 0;
     bool rpar_cons_seq = false;   // transRNorm per relation, a chain of chunks (kernels_transr_seq.hpp)
     size_t rpar_seq_lds = 0;
+    DevBuf rpar_vio;              // the n <= 64 chain kernels' violator slots (in-kernel pair records)
     bool rpar_cons_wide = false;  // the same chain for n <= 112 off the n <= 64 matrix-core path (kernels_transr_chainw.hpp)
     size_t rpar_wide_lds = 0;
     DevBuf rpar_pflag, rpar_cons_tile, rpar_cpairs, rpar_cnrows;
@@ -1236,8 +1237,6 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
         return KB2E_EINVAL;
     if (g.model == KB2E_TRANSR && g.num_relations > g.num_entities) return KB2E_EINVAL;
     if (g.schedule == KB2E_SCHEDULE_PARALLEL && g.model == KB2E_TRANSR && g.dim > 128) return KB2E_EUNSUPPORTED;  // entityVec_next_[relation]
-    if (g.model == KB2E_TRANSR && ((size_t)g.dim * (g.dim + 1) + 3 * (size_t)g.dim) * (g.precision / 8) > 152 * 1024)
-        return KB2E_EUNSUPPORTED;  // the owner's relation matrix must fit in LDS
     std::unique_ptr<kb2e_ctx> c(new kb2e_ctx());
     c->cfg = g;
     c->rng.seed_with(g.seed);
@@ -1288,6 +1287,12 @@ const char* kb2e_last_error(const kb2e_ctx* ctx) { return ctx ? ctx->err.c_str()
 kb2e_status kb2e_upload_triples(kb2e_ctx* c, const int32_t* h, const int32_t* t, const int32_t* r, int64_t count) {
     return guarded(c, [&] {
         if (!h || !t || !r || count < 1) return fail(c, KB2E_EINVAL, "empty triple set");
+        {  // ORDERED TransR training: the relation owner's matrix must fit in LDS (evaluation has no such limit)
+            const kb2e_config& g = c->cfg;
+            if (g.model == KB2E_TRANSR && g.schedule == KB2E_SCHEDULE_ORDERED &&
+                ((size_t)g.dim * (g.dim + 1) + 3 * (size_t)g.dim) * (g.precision / 8) > 152 * 1024)
+                return fail(c, KB2E_EUNSUPPORTED, "ORDERED TransR trains dim <= 138 (FP64) / 195 (FP32)");
+        }
         HIPCHK(hipSetDevice(c->cfg.device));
         c->ts.build(h, t, r, count, c->cfg.num_entities, c->cfg.num_relations);
         c->heads.alloc(count * 4);

@@ -17,21 +17,24 @@
 // Why a second kernel.  The n <= 64 kernels keep K0's column c in lane c of one
 // wave (4 KS registers) and take their pair lists from the matrix-core gradient
 // kernel.  At n = 100 (K5, BASELINE configs[4]) a column of K0 is 100 doubles,
-// W_c alone is 91 KB of LDS, and the VALU tile path has no compacted pair lists.
-// Here:
-//  * the workgroup is one relation segment of the batch's event index; it finds
-//    the relation's last active sample, then builds its pair list in windows of
-//    256 samples (a thread a sample: its four slots, first occurrences by the
-//    per-batch (relation, entity) table, a block scan for the positions); the
-//    last update's slots are held back for the tail, so the tail is exact
-//    however many windows the relation spans;
-//  * K0 lives in registers spread over all four waves: thread t < 2 NP holds
-//    rows [h NP/2, (h + 1) NP/2) of column c = t >> 1 (h = t & 1), so V = p K0 is
-//    NP/2 FMAs a thread (p broadcast from LDS) and one lane-pair DPP add;
-//  * per chunk of 16 pairs the four waves make P = A W_c and the Gram matrix
-//    A A^T on the matrix cores (v_mfma_f64_16x16x4, runtime k-steps); the walk
-//    is workgroup-wide, three barriers a violator (the p.V / V.V partial sums,
-//    g, then the later pairs' P_j -= lr (a_j . a_v) g and |p_j|^2 afresh);
+// W_c alone is 100 KB of LDS, and the VALU tile path has no compacted pair lists.
+// Here, eight waves a workgroup (one workgroup a CU: the LDS):
+//  * the workgroup is one relation of the batch, the most frequent relations
+//    first; it finds the relation's last active sample, then builds its pair list
+//    in windows of 512 samples (a thread a sample: its four slots, first
+//    occurrences by the per-batch (relation, entity) table, a block scan for the
+//    positions); the last update's slots are held back for the tail, so the tail
+//    is exact however many windows the relation spans;
+//  * K0 lives in registers spread over the waves: thread t < 4 NP holds rows
+//    [h NP/4, (h + 1) NP/4) of column c = t >> 2 (h = t & 3), so V = p K0 is NP/4
+//    FMAs a thread (p broadcast from LDS) and two quad DPP adds; the W_c update
+//    of a violator is the same layout (NP/4 rows of one column a thread, in
+//    registers, eight rows at a time);
+//  * per chunk of 16 pairs P = A W_c (NB column tiles) and the Gram matrix A A^T
+//    (one tile) on the matrix cores, a tile a wave (NB + 1 <= 8), NP / 4 k-steps
+//    over zero padding; the walk is workgroup-wide, three barriers a violator
+//    (the p.V / V.V partial sums, g, then the later pairs'
+//    P_j -= lr (a_j . a_v) g and |p_j|^2 afresh);
 //  * the next chunk's entity rows are loaded into registers while the current
 //    chunk is walked.
 #pragma once
@@ -40,29 +43,37 @@
 
 namespace kb2e {
 
+constexpr int kWideThreads = 512;     // eight waves
+constexpr int kWideWaves = kWideThreads / 64;
 constexpr int kWideRows = 16;         // pairs a chunk: one MFMA row tile
-constexpr int kWideWin = 256;         // samples a window (a thread each)
+constexpr int kWideWin = kWideThreads;  // samples a window (a thread each)
 constexpr int kWidePairs = 4 * kWideWin;
 
 __host__ __device__ constexpr int wide_nb(int n) { return (n + 15) / 16; }
 
-// LDS bytes: W_c [NK][LW] | A [R][LW] | P [R][LW] | Gram [R][R + 1] | qpart [NB][R] |
-// red [4][2] ; ints: pair entities, slots [kWidePairs] | wave sums [4] | misc [8] ; vio flags [kWidePairs]
+// LDS bytes: W_c [NP][LW] | A [R][LW] | P [R][LW] | Gram [R][R + 1] | qpart [NB][R] |
+// red [8][2] ; ints: pair entities, slots [kWidePairs] | wave sums [8] | misc [8] ; vio flags [kWidePairs]
+// (W_c and A zero padded to NP x NP and R x NP: the MFMA k-loop runs NP / 4 steps, no guards)
 __host__ __device__ constexpr size_t chainw_lds(int n) {
-    return sizeof(double) * ((size_t)((n + 3) / 4 * 4) * (16 * wide_nb(n) + 2) +
+    return sizeof(double) * ((size_t)(16 * wide_nb(n)) * (16 * wide_nb(n) + 2) +
                              2 * (size_t)kWideRows * (16 * wide_nb(n) + 2) + (size_t)kWideRows * (kWideRows + 1) +
-                             (size_t)wide_nb(n) * kWideRows + 8) +
-           sizeof(int) * (2 * (size_t)kWidePairs + 4 + 8) + (size_t)kWidePairs;
+                             (size_t)wide_nb(n) * kWideRows + 2 * kWideWaves) +
+           sizeof(int) * (2 * (size_t)kWidePairs + kWideWaves + 8) + (size_t)kWidePairs;
 }
 
-// lane l + (l ^ 1): the two halves of a column pair
-__device__ __forceinline__ double lane_pair_sum(double x) { return x + dpp_mov<0xB1>(x); }  // quad_perm [1,0,3,2]
+// the sum over the four lanes of a quad (lanes 4q .. 4q + 3), in every lane of it
+__device__ __forceinline__ double quad_sum(double x) {
+    x += dpp_mov<0xB1>(x);  // quad_perm [1,0,3,2]
+    return x + dpp_mov<0x4E>(x);  // quad_perm [2,3,0,1]
+}
 
 template <int NB>
-__global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a, RParBufs<double> bf) {
+__global__ __launch_bounds__(kWideThreads) void transr_cons_chain_wide_kernel(RParArgs a, RParBufs<double> bf) {
     using T = double;
     using M = Mfma16<T>;
-    constexpr int NP = 16 * NB, LW = NP + 2, R = kWideRows, LG = R + 1, KH = NP / 2;
+    constexpr int NP = 16 * NB, LW = NP + 2, R = kWideRows, LG = R + 1, KQ = NP / 4;
+    constexpr int NT = kWideThreads, NW = kWideWaves;
+    static_assert(NB + 1 <= NW, "a tile a wave");
     // block b takes the b-th most frequent relation, so the long chains of the hot
     // relations start first (a hot relation dispatched late would add its wait to the
     // batch); its segment in this batch's index by binary search over the batch's
@@ -81,23 +92,23 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
         if (a.seg_row[lo] != want) return;
         s = lo;
     }
-    const int n = a.n, ld = a.ld, KS = (n + 3) / 4, NK = 4 * KS;
+    const int n = a.n, ld = a.ld;
     const int p0 = a.seg_start[s], ns = (a.seg_start[s + 1] - p0) / 2;
     const int tid = threadIdx.x, w = tid >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
-    const int c = tid >> 1, h = tid & 1;  // K0 / V / W-update layout: column c, half h of the rows
-    const bool colt = c < NP;             // (2 NP <= 256 threads)
+    const int c = tid >> 2, h = tid & 3;  // K0 / V / W-update layout: column c, quarter h of the rows
+    const bool colt = c < NP;             // (4 NP <= 512 threads)
     const T lr = (T)a.lr;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    T* Wc = (T*)smem;            // [NK][LW]
-    T* A = Wc + NK * LW;         // [R][LW] the chunk's entity rows
+    T* Wc = (T*)smem;            // [NP][LW]
+    T* A = Wc + NP * LW;         // [R][LW] the chunk's entity rows
     T* P = A + R * LW;           // [R][LW] projections; the violators' rows then hold G
     T* Gm = P + R * LW;          // [R][LG]
     T* qpart = Gm + R * LG;      // [NB][R]
-    T* red = qpart + NB * R;     // [4][2]
-    int* pe = (int*)(red + 8);   // [kWidePairs]
+    T* red = qpart + NB * R;     // [NW][2]
+    int* pe = (int*)(red + 2 * NW);  // [kWidePairs]
     int* ps = pe + kWidePairs;   // [kWidePairs]
-    int* wsum = ps + kWidePairs; // [4]
-    int* misc = wsum + 4;        // [8]
+    int* wsum = ps + kWidePairs; // [NW]
+    int* misc = wsum + NW;       // [8]
     uint8_t* vflag = (uint8_t*)(misc + 8);  // [kWidePairs]
     const long long ck0 = clock64();
     unsigned long long n_chunks = 0, n_vio = 0, n_rounds = 0, max_m = 0;
@@ -106,7 +117,8 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
     // 1 window list, 2 rows + A barrier, 3 P / Gram MFMA + B1, 4 |p|^2 + K0, 5 V + sums,
     // 6 barrier (1), 7 rounds + g, 8 barrier (2), 9 later pairs, 10 barrier (3), 11 records +
     // W update, 12 end-of-chunk barrier, 13 window flags, 14 tail, 15 write-back
-    unsigned long long ph[16] = {};
+    __shared__ unsigned long long ph[16];  // (in LDS: sixteen 64-bit registers are too dear here)
+    if (tid < 16) ph[tid] = 0;
     long long tq = ck0;
     auto tick = [&](int k) {
         if (bf.stats && tid == 0) {
@@ -116,10 +128,10 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
         }
     };
 
-    // the relation's last active sample (from the end, 256 samples a round)
+    // the relation's last active sample (from the end, NT samples a round)
     if (tid == 0) misc[0] = -1;
     __syncthreads();
-    for (int qb = ns - kWideWin;; qb -= kWideWin) {
+    for (int qb = ns - NT;; qb -= NT) {
         const int q = qb + tid;
         const bool act = q >= 0 && q < ns && a.act[a.kl.kk_of(a.keys[p0 + 2 * q])];
         const uint64_t b = __ballot(act);
@@ -134,33 +146,35 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
     const int kl = a.kl.kk_of(a.keys[p0 + 2 * klq]);
     const bool has_rel = r < a.ne && ptab_first(a, r, r) < 0;  // (entity'[r], r), transr/trainer.cpp:187
 
-    // W'_r, zero padded to NK x NP
-    for (int idx = tid; idx < NK * NP; idx += 256) {
+    // W'_r, zero padded to NP x NP
+    for (int idx = tid; idx < NP * NP; idx += NT) {
         const int j = idx / NP, i = idx % NP;
         Wc[j * LW + i] = (j < n && i < n) ? bf.W[((int64_t)r * n + j) * ld + i] : T(0);
     }
-    T k0[KH];
+    T k0[KQ];
 #pragma unroll
-    for (int i = 0; i < KH; ++i) k0[i] = T(0);
+    for (int i = 0; i < KQ; ++i) k0[i] = T(0);
     bool have_k0 = false, changed = false;
     tick(0);
 
-    // the chunk's rows: R x NP elements, NB a thread, into registers (every load is
+    // the chunk's rows: R x NP elements, RPT a thread, into registers (every load is
     // issued, padding zeroed when stored: no register written under a branch while a
     // load into it is in flight)
-    T rows[NB];
+    constexpr int RPT = (R * NP + NT - 1) / NT;
+    T rows[RPT];
     uint32_t rows_ok = 0;
     auto load_rows = [&](int b, int e) {
-        int ent[NB];
+        int ent[RPT];
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-            const int f = b + (tid + q * 256) / NP;
-            ent[q] = f < e ? pe[f] : -1;
+        for (int q = 0; q < RPT; ++q) {
+            const int idx = tid + q * NT;
+            const int f = b + idx / NP;
+            ent[q] = idx < R * NP && f < e ? pe[f] : -1;
         }
         rows_ok = 0;
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-            const int j = (tid + q * 256) % NP;
+        for (int q = 0; q < RPT; ++q) {
+            const int j = (tid + q * NT) % NP;
             const bool ok = ent[q] >= 0 && j < n;
             rows[q] = bf.ent[ok ? (uint32_t)ent[q] * (uint32_t)ld + (uint32_t)j : 0u];
             rows_ok |= (ok ? 1u : 0u) << q;
@@ -168,9 +182,9 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
     };
     auto store_rows = [&]() {
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-            const int idx = tid + q * 256;
-            A[(idx / NP) * LW + idx % NP] = ((rows_ok >> q) & 1) ? rows[q] : T(0);
+        for (int q = 0; q < RPT; ++q) {
+            const int idx = tid + q * NT;
+            if (idx < R * NP) A[(idx / NP) * LW + idx % NP] = ((rows_ok >> q) & 1) ? rows[q] : T(0);
         }
     };
 
@@ -182,22 +196,39 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
         __syncthreads();  // A (and W_c) ready
         if (nb < ne) load_rows(nb, ne);
         tick(2);
-        // P = A W_c (NB column tiles) and the Gram tile, dealt round the waves
-        for (int tl = w; tl <= NB; tl += 4) {
-            const bool gram = tl == NB;
+        // P = A W_c (NB column tiles) and the Gram tile A A^T (its B operand is the A
+        // operand itself), a tile a wave; NP / 4 k-steps over the zero padding,
+        // straight-line, four k-steps' fragments a block
+        if (w <= NB) {
+            const bool gram = w == NB;
+            const T* ap = A + l16 * LW + kq;
+            const T* bp = gram ? ap : Wc + kq * LW + w * 16 + l16;
+            const int bstep = gram ? 4 : 4 * LW;
             typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
-            for (int kb = 0; kb < KS; kb += 8) {
-                T av[8], bv[8];
+            // blocks of four k-steps, the next block's fragments loaded during this one's MFMAs
+            T av[4], bv[4];
 #pragma unroll
-                for (int s8 = 0; s8 < 8; ++s8) {
-                    const int k = 4 * (kb + s8) + kq;
-                    const bool ok = kb + s8 < KS;
-                    av[s8] = ok ? A[l16 * LW + k] : T(0);
-                    bv[s8] = ok ? (gram ? A[l16 * LW + k] : Wc[k * LW + tl * 16 + l16]) : T(0);
+            for (int s4 = 0; s4 < 4; ++s4) {
+                av[s4] = ap[4 * s4];
+                bv[s4] = bp[bstep * s4];
+            }
+#pragma unroll 1
+            for (int kb = 0; kb < NP / 4; kb += 4) {
+                T an[4], bn[4];
+                if (kb + 4 < NP / 4) {
+#pragma unroll
+                    for (int s4 = 0; s4 < 4; ++s4) {
+                        an[s4] = ap[4 * (kb + 4 + s4)];
+                        bn[s4] = bp[bstep * (kb + 4 + s4)];
+                    }
                 }
 #pragma unroll
-                for (int s8 = 0; s8 < 8; ++s8)
-                    if (kb + s8 < KS) acc = M::mma(av[s8], bv[s8], acc);
+                for (int s4 = 0; s4 < 4; ++s4) acc = M::mma(av[s4], bv[s4], acc);
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4) {
+                    av[s4] = an[s4];
+                    bv[s4] = bn[s4];
+                }
             }
             if (gram) {
 #pragma unroll
@@ -206,13 +237,13 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
                 T sp[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    P[(kq + 4 * q) * LW + tl * 16 + l16] = acc[q];
+                    P[(kq + 4 * q) * LW + w * 16 + l16] = acc[q];
                     sp[q] = acc[q] * acc[q];
                 }
                 row16_sums<T, 4>(sp);
                 if (l16 == 0) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) qpart[tl * R + kq + 4 * q] = sp[q];
+                    for (int q = 0; q < 4; ++q) qpart[w * R + kq + 4 * q] = sp[q];
                 }
             }
         }
@@ -220,23 +251,27 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
         tick(3);
         const int j = l16;  // |p_j|^2 of pair j in lanes j, j + 16, ... of every wave
         T qj = T(0);
-        if (j < cc) {
-            qj = qpart[j];
-            for (int v = 1; v < NB; ++v) qj += qpart[v * R + j];
+        {
+            T qv[NB];
+#pragma unroll
+            for (int v = 0; v < NB; ++v) qv[v] = qpart[v * R + j];
+#pragma unroll
+            for (int v = 0; v < NB; ++v) qj += qv[v];
+            if (j >= cc) qj = T(0);
         }
         uint32_t cand = (uint32_t)__ballot(l < R && j < cc && qj > T(1));
         if (!cand) {
             tick(4);
             return;
         }
-        if (!have_k0) {  // K0[:, c] rows of half h = sum_j W[j][i] W[j][c] (W_c is still W'_r)
+        if (!have_k0) {  // K0[:, c] rows of quarter h = sum_j W[j][i] W[j][c] (W_c is still W'_r)
             have_k0 = true;
             if (colt) {
                 for (int jr = 0; jr < n; ++jr) {
                     const T wc = Wc[jr * LW + c];
-                    const double2* wrow = (const double2*)(Wc + jr * LW + h * KH);
+                    const double2* wrow = (const double2*)(Wc + jr * LW + h * KQ);
 #pragma unroll
-                    for (int i2 = 0; i2 < KH / 2; ++i2) {
+                    for (int i2 = 0; i2 < KQ / 2; ++i2) {
                         const double2 x = wrow[i2];
                         k0[2 * i2] = fma(x.x, wc, k0[2 * i2]);
                         k0[2 * i2 + 1] = fma(x.y, wc, k0[2 * i2 + 1]);
@@ -251,21 +286,27 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
             cand &= ~((1u << cursor) - 1);
             if (!cand) break;
             const int v = __builtin_ctz(cand);
-            // V_c = sum_i p_v[i] K0[i][c], the two halves of the rows in lanes 2c, 2c + 1
+            // V_c = sum_i p_v[i] K0[i][c], the quarters of the rows in the lanes of a quad
             T V = T(0), pv = T(0);
             if (colt) {
                 T acc4[4] = {T(0), T(0), T(0), T(0)};
-                const double2* prow = (const double2*)(P + v * LW + h * KH);
+                const double2* prow = (const double2*)(P + v * LW + h * KQ);
+                pv = P[v * LW + c];
 #pragma unroll
-                for (int i2 = 0; i2 < KH / 2; ++i2) {
-                    const double2 x = prow[i2];
-                    acc4[(2 * i2) & 3] = fma(x.x, k0[2 * i2], acc4[(2 * i2) & 3]);
-                    acc4[(2 * i2 + 1) & 3] = fma(x.y, k0[2 * i2 + 1], acc4[(2 * i2 + 1) & 3]);
+                for (int i0 = 0; i0 < KQ / 2; i0 += NB) {  // NB double2 loads in flight a block
+                    double2 pr[NB];
+#pragma unroll
+                    for (int i2 = 0; i2 < NB; ++i2) pr[i2] = prow[i0 + i2];
+#pragma unroll
+                    for (int i2 = 0; i2 < NB; ++i2) {
+                        const int i = 2 * (i0 + i2);
+                        acc4[i & 3] = fma(pr[i2].x, k0[i], acc4[i & 3]);
+                        acc4[(i + 1) & 3] = fma(pr[i2].y, k0[i + 1], acc4[(i + 1) & 3]);
+                    }
                 }
                 V = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
-                pv = P[v * LW + c];
             }
-            V = lane_pair_sum(V);
+            V = quad_sum(V);
             T s2[2] = {colt && h == 0 ? pv * V : T(0), colt && h == 0 ? V * V : T(0)};
             wave_sums<T, 2>(s2);
             if (l == 0) {
@@ -275,8 +316,17 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
             tick(5);
             __syncthreads();  // (1) the partial sums
             tick(6);
-            const T pV = (red[0] + red[2]) + (red[4] + red[6]);
-            const T VV = (red[1] + red[3]) + (red[5] + red[7]);
+            T pV = T(0), VV = T(0);
+            {
+                T rr[2 * NW];
+#pragma unroll
+                for (int k = 0; k < 2 * NW; ++k) rr[k] = red[k];
+#pragma unroll
+                for (int k = 0; k < NW; ++k) {
+                    pV += rr[2 * k];
+                    VV += rr[2 * k + 1];
+                }
+            }
             const T pp = readlane_f(qj, v);
             const T aa = Gm[v * LG + v];  // |a_v|^2
             const T pvd = pV + aa * pp, vvd = VV + T(2) * aa * pV + aa * aa * pp;
@@ -293,18 +343,23 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
             tick(7);
             __syncthreads();  // (2) g in P's row v
             tick(8);
-            {  // the later pairs: P[jr] -= lr (a_jr . a_v) g, |p_jr|^2 afresh (16 lanes a row)
+            if (tid < 16 * R) {  // the later pairs: P[jr] -= lr (a_jr . a_v) g, |p_jr|^2 afresh (16 lanes a row)
                 const int jr = tid >> 4, s16 = tid & 15;
                 const bool later = jr > v && jr < cc;
                 if (later) {
                     const T gl = -lr * Gm[jr * LG + v];
+                    T x[NB], g[NB];
+#pragma unroll
+                    for (int k = 0; k < NB; ++k) {
+                        x[k] = P[jr * LW + s16 + 16 * k];
+                        g[k] = P[v * LW + s16 + 16 * k];
+                    }
                     T sq = T(0);
 #pragma unroll
                     for (int k = 0; k < NB; ++k) {
-                        const int ci = s16 + 16 * k;
-                        const T x = fma(gl, P[v * LW + ci], P[jr * LW + ci]);
-                        P[jr * LW + ci] = x;
-                        sq = fma(x, x, sq);
+                        x[k] = fma(gl, g[k], x[k]);
+                        P[jr * LW + s16 + 16 * k] = x[k];
+                        sq = fma(x[k], x[k], sq);
                     }
                     T sv[1] = {sq};
                     row16_sums<T, 1>(sv);
@@ -334,18 +389,31 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
                 if (sl < 0) bf.relpair_stamp[r] = bf.stamp;
             }
         }
-        if (colt && c < n) {  // (rows of half h of column c: this thread's alone)
-            const int k1 = min(n, (h + 1) * KH);
-            for (uint32_t mm = vmask; mm; mm &= mm - 1) {
-                const int v = __builtin_ctz(mm);
-                const T gl = -lr * P[v * LW + c];
-                for (int k = h * KH; k < k1; ++k) Wc[k * LW + c] = fma(A[v * LW + k], gl, Wc[k * LW + c]);
+        if (colt && c < n) {  // rows of quarter h of column c (this thread's alone), four at a time in registers
+#pragma unroll
+            for (int k0r = 0; k0r < KQ; k0r += 4) {
+                const int k = h * KQ + k0r;
+                T wv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) wv[u] = Wc[(k + u) * LW + c];
+                for (uint32_t mm = vmask; mm; mm &= mm - 1) {
+                    const int v = __builtin_ctz(mm);
+                    const T gl = -lr * P[v * LW + c];
+                    const double2* ar = (const double2*)(A + v * LW + k);
+                    const double2 a0 = ar[0], a1 = ar[1];
+                    wv[0] = fma(a0.x, gl, wv[0]);
+                    wv[1] = fma(a0.y, gl, wv[1]);
+                    wv[2] = fma(a1.x, gl, wv[2]);
+                    wv[3] = fma(a1.y, gl, wv[3]);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) Wc[(k + u) * LW + c] = wv[u];
             }
         }
         tick(11);
     };
 
-    // windows of 256 samples up to the last active one; the last update's slots wait for the tail
+    // windows of NT samples up to the last active one; the last update's slots wait for the tail
     for (int wq = 0; wq <= klq; wq += kWideWin) {
         const int q = wq + tid;
         int kk = -1, ents[4] = {-1, -1, -1, -1};
@@ -379,9 +447,13 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
         }
         if (l == kWave - 1) wsum[w] = x;
         __syncthreads();
-        int off = 0;
-        for (int k = 0; k < w; ++k) off += wsum[k];
-        const int npw = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+        int off = 0, npw = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            const int ws = wsum[k];
+            off += k < w ? ws : 0;
+            npw += ws;
+        }
         const int pos0 = off + x - cnt;
         {
             int pos = pos0;
@@ -448,15 +520,14 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
         }
     }
     if (ntail > 0) {
-        if (changed) {  // the last update's unit rows (transr/trainer.cpp:178-180)
+        if (changed) {  // the last update's unit rows (transr/trainer.cpp:178-180): row c, quarter h of the columns
             const int jr = c;
             T sq = T(0);
             if (colt && jr < n)
-                for (int i = h * KH; i < min(n, (h + 1) * KH); ++i) sq = fma(Wc[jr * LW + i], Wc[jr * LW + i], sq);
-            const T len = sqrt(lane_pair_sum(sq));
-            __syncthreads();
+                for (int i = h * KQ; i < min(n, (h + 1) * KQ); ++i) sq = fma(Wc[jr * LW + i], Wc[jr * LW + i], sq);
+            const T len = sqrt(quad_sum(sq));
             if (colt && jr < n)
-                for (int i = h * KH; i < min(n, (h + 1) * KH); ++i) Wc[jr * LW + i] = Wc[jr * LW + i] / len;
+                for (int i = h * KQ; i < min(n, (h + 1) * KQ); ++i) Wc[jr * LW + i] = Wc[jr * LW + i] / len;
         }
         __syncthreads();  // the tail list and W_c
         load_rows(0, ntail);
@@ -469,7 +540,7 @@ __global__ __launch_bounds__(256) void transr_cons_chain_wide_kernel(RParArgs a,
     }
     tick(14);
     // the relation's matrix back
-    for (int idx = tid; idx < n * n; idx += 256) {
+    for (int idx = tid; idx < n * n; idx += NT) {
         const int j = idx / n, i = idx % n;
         bf.W[((int64_t)r * n + j) * ld + i] = Wc[j * LW + i];
     }

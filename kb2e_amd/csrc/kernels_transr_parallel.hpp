@@ -177,6 +177,8 @@ struct RParBufs {
     int32_t dbg;         // transRNorm wave kernel: phases skipped for timing experiments (tools; wrong results)
     int32_t chain_list;  // pipelined chain kernel: pairs a window (0: all that fit the LDS; tests force windows)
     int32_t chain_tiles; // chain kernels: tiles a window (0: the prefix table's 256; tests force windows)
+    int32_t* vio;        // n <= 64 chain kernels: [tiles][kCPairs] the violators' slots of the relation whose
+                         // first tile it is (-2: (entity[r], r)); its pair records are made in-kernel
 };
 
 __host__ __device__ constexpr int rm_up16_host_dev(int v) { return (v + 15) & ~15; }

@@ -47,10 +47,8 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
     constexpr int NH = NP / 2;              // columns of a row half (walk registers)
     static_assert(2 * R * L >= NP * L, "the K0 image borrows the two P buffers");
     const int t0 = a.batch_t0[a.batch], t1 = a.batch_t0[a.batch + 1];
-    const int g0 = blockIdx.x;
-    if (t0 + g0 >= t1) return;
-    const int r = a.td_r[t0 + g0];
-    if (g0 > 0 && a.td_r[t0 + g0 - 1] == r) return;  // not the relation's first tile
+    int g0, r;  // the relation's first tile within the batch
+    if (!chain_first_tile(a, t0, t1, g0, r)) return;
     const int n = a.n, ld = a.ld;
     const int w = threadIdx.x >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
     const bool mine = w < NB;  // this wave owns a column slice (K0, the W_c update)
@@ -153,6 +151,8 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
         __syncthreads();  // the P buffers are free again
     }
     bool changed = false;
+    int32_t* const vio = bf.vio + (int64_t)g0 * kCPairs;  // the relation's violators (run * kCPairs >= its pairs)
+    int nvt = 0;
     tick(0);
 
     // one 16 x 16 MFMA tile: rows rt of A (Ar) against Wc columns cb (gram = false)
@@ -497,13 +497,15 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
             const bool restart = nbase == tail_start && changed && cn > 0;  // the tail: afresh
             if (cn > 0 && !restart) correct_q(Pn, cn, nv, P);
             tick(14);
-            if (vmask) {  // the violators' pair records G (da = -lr W G made later), a wave each
+            if (vmask) {  // the violators' pair records G (da = -lr W G at the end), a wave each
                 for (int k = w; k < nv; k += kChainThreads / kWave) {
                     const int v = vlist[k];
                     const int sl = ps[base + v];
                     T* dst = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
                     if (l < n) dst[l] = P[v * L + l];
+                    if (l == 0) vio[nvt + k] = sl;
                 }
+                nvt += nv;
             }
             tick(15);
             __syncthreads();  // B2
@@ -522,6 +524,8 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
     // the relation's matrix back: each wave its column slice
     if (mine && col < n)
         for (int jj = 0; jj < n; ++jj) bf.W[((int64_t)r * n + jj) * ld + col] = Wc[jj * L + col];
+    __syncthreads();  // (the last records written; the P buffers free)
+    chain_records<T, NP, L>(a, bf, r, vio, nvt, Wc, Pbuf);
     if (bf.stats) {
         if (threadIdx.x == 0) {
             const unsigned long long cyc = (unsigned long long)(clock64() - ck0);

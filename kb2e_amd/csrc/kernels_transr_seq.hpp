@@ -135,6 +135,55 @@ __device__ __forceinline__ int transr_rounds_violator(T Q0, T w2, T eps, T rho, 
     return m;
 }
 
+// The chain kernels' block -> relation map: block b takes the b-th most frequent
+// relation (a.rel_order), so the hot relations' long chains start first instead
+// of waiting for a dispatch slot behind short ones; its first tile g0 within the
+// batch by binary search over the batch's tile relations (tiles follow the
+// relation segments, sorted by relation).  False: the relation is not in the batch.
+__device__ __forceinline__ bool chain_first_tile(const RParArgs& a, int t0, int t1, int& g0, int& r) {
+    r = a.rel_order[blockIdx.x];
+    int lo = t0, hi = t1;  // first tile with td_r >= r
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a.td_r[mid] < r) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo >= t1 || a.td_r[lo] != r) return false;
+    g0 = lo - t0;
+    return true;
+}
+
+// The relation's pair records G -> da = -lr W G with its final matrix
+// (transr/trainer.cpp:59-60; first order in lr the same as the matrix at the
+// pair's chunk), at the end of its chain: the nvt violator slots in vio (written
+// during the chain), W_c in LDS (stride L), `stage` [4][L] free LDS.  A wave a
+// record: the G row staged in LDS, lane j makes da_j = sum_i W[j][i] G_i (four
+// chains).  (Made here, the records of the ~440 relations that finish early
+// overlap the hottest relation's chain instead of following it in a kernel of
+// their own.)
+template <typename T, int NP, int L>
+__device__ __forceinline__ void chain_records(const RParArgs& a, const RParBufs<T>& bf, int r, const int32_t* vio,
+                                              int nvt, const T* Wc, T* stage) {
+    const int n = a.n, ld = a.ld, w = threadIdx.x >> 6, l = lane_id();
+    T* gs = stage + w * L;
+    const int nw = blockDim.x >> 6;
+    for (int k = w; k < nvt; k += nw) {
+        const int sl = vio[k];
+        T* row = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
+        if (l < NP) gs[l] = l < n ? row[l] : T(0);
+        wave_lds_sync();
+        T acc[4] = {T(0), T(0), T(0), T(0)};
+        const int j = l < NP ? l : 0;
+#pragma unroll
+        for (int i = 0; i < NP; i += 4)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[u] = fma(Wc[j * L + i + u], gs[i + u], acc[u]);
+        const T da = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        wave_lds_sync();  // (every lane has read the staged row before the next one lands)
+        if (l < n) row[l] = -(T)a.lr * da;
+    }
+}
+
 // KS = ceil(n / 4): the live k-steps of a contraction over n, a compile-time
 // count so that the MFMA chains are straight-line code (no per-step branches)
 template <typename T, int KS>
@@ -144,10 +193,8 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
     constexpr int NB = (4 * KS + 15) / 16;  // column slices of 16
     constexpr int NP = 16 * NB, L = NP + 2, R = kChainRows, LG = R + 1;
     const int t0 = a.batch_t0[a.batch], t1 = a.batch_t0[a.batch + 1];
-    const int g0 = blockIdx.x;  // tile index within the batch
-    if (t0 + g0 >= t1) return;
-    const int r = a.td_r[t0 + g0];
-    if (g0 > 0 && a.td_r[t0 + g0 - 1] == r) return;  // not the relation's first tile
+    int g0, r;  // the relation's first tile within the batch
+    if (!chain_first_tile(a, t0, t1, g0, r)) return;
     const int n = a.n, ld = a.ld;
     const int w = threadIdx.x >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
     const bool mine = w < NB;  // this wave owns a column slice (K0, the W_c update)
@@ -224,6 +271,8 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
     __syncthreads();
     const int run = misc[5], has_rel = misc[3], g_tail = misc[4], n_tail = misc[6];
     bool have_k0 = false, changed = false;
+    int32_t* const vio = bf.vio + (int64_t)g0 * kCPairs;  // the relation's violators (run * kCPairs >= its pairs)
+    int nvt = 0;
     T k0c[4 * KS];  // wave 0: K0's column l (the violators' V rows), loaded once K0 is made
     tick(0);
     int chunk_no = 0;  // chunks so far (row buffer parity)
@@ -525,7 +574,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
             tick(5);
             if (anyv) {
                 const uint32_t vmask = (uint32_t)misc[1];
-                {  // the violators' pair records G (da = -lr W G made later), a wave each
+                {  // the violators' pair records G (da = -lr W G at the end), a wave each
                     uint32_t mm = vmask;
                     for (int k = 0; k < w && mm; ++k) mm &= mm - 1;
                     while (mm) {
@@ -533,8 +582,10 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
                         const int sl = ps[base + v];
                         T* dst = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
                         if (l < n) dst[l] = P[v * L + l];
+                        if (l == 0) vio[nvt + __builtin_popcount(vmask & ((1u << v) - 1u))] = sl;
                         for (int k = 0; k < 4 && mm; ++k) mm &= mm - 1;
                     }
+                    nvt += __builtin_popcount(vmask);
                 }
                 // W_c[:, slice] -= lr sum_v A[v]^T G[v] over the chunk's violators
                 if (vmask) changed = true;
@@ -562,6 +613,8 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
     // the relation's matrix back: each wave its column slice (the transRNorm pass adds no partials)
     if (mine && col < n)
         for (int jj = 0; jj < n; ++jj) bf.W[((int64_t)r * n + jj) * ld + col] = Wc[jj * L + col];
+    __syncthreads();  // (the last records written; P free)
+    chain_records<T, NP, L>(a, bf, r, vio, nvt, Wc, P);
     if (bf.stats) {
         if (threadIdx.x == 0) {
             const unsigned long long cyc = (unsigned long long)(clock64() - ck0);

@@ -102,10 +102,11 @@ void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, int grid, si
     RParBufs<double> bb = bf;
     void* args[] = {&aa, &bb};
     // (the LDS size was chosen by cons_seq_setup under the same switch)
-    HIPCHK(hipLaunchKernel(lds == pipe_lds<double>(a.n) && use_pipe() ? pipe_fn(a.n) : chain_fn(a.n), dim3(grid),
+    // one workgroup per relation, most frequent first (chain_first_tile; those absent exit)
+    (void)grid;
+    // (the pair records are made at the end of each relation's chain: chain_records)
+    HIPCHK(hipLaunchKernel(lds == pipe_lds<double>(a.n) && use_pipe() ? pipe_fn(a.n) : chain_fn(a.n), dim3(a.nr),
                            dim3(kChainThreads), args, lds, stream));
-    const int da_grid = (int)(((int64_t)4 * a.B + a.nr + 3) / 4);  // a wave a record
-    HIPCHK(hipLaunchKernel((const void*)transr_cons_da_kernel<double>, dim3(da_grid), dim3(256), args, 0, stream));
 }
 
 bool cons_chainw_supported(int n) { return n >= 1 && n <= kWideMaxN; }
@@ -122,7 +123,7 @@ void cons_chainw_launch(const RParArgs& a, const RParBufs<double>& bf, size_t ld
     void* args[] = {&aa, &bb};
     // one workgroup per relation, most frequent first (those absent from the batch exit)
     const int grid = a.nr;
-    HIPCHK(hipLaunchKernel(chainw_fn(a.n), dim3(grid), dim3(256), args, lds, stream));
+    HIPCHK(hipLaunchKernel(chainw_fn(a.n), dim3(grid), dim3(kWideThreads), args, lds, stream));
     const int da_grid = (int)(((int64_t)4 * a.B + a.nr + 3) / 4);  // a wave a record
     HIPCHK(hipLaunchKernel((const void*)transr_cons_da_wide_kernel, dim3(da_grid), dim3(256), args, 0, stream));
 }

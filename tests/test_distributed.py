@@ -1,4 +1,4 @@
-"""Multi-rank path on CPU (gloo, world size 2 and 3): head-hash sharding and the
+"""Multi-rank path on CPU (gloo, world size 2, 3 and 4): head-hash sharding and the
 epoch-boundary merge of kb2e_amd.distributed (reduce-scatter of entity deltas
 to block owners + all-gather, all-reduce of relation/weight deltas, changed
 rows renormalised) against numpy renorm(T0 + sum_r (T_r - T0))."""
@@ -87,7 +87,7 @@ def _worker(rank, world, port, out):
 
 
 @pytest.mark.timeout(120)
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_merge_matches_numpy_renorm_of_summed_deltas(world):
     mgr = mp.Manager()
     out = mgr.dict()
