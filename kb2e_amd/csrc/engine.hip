@@ -154,6 +154,8 @@ struct kb2e_ctx {
     DevBuf hpar_orth;                      // PARALLEL TransH: orthogonality flags per sample
     DevBuf hpar_tag;                       // PARALLEL TransH: per entity, the relations its flagged pairs have
     uint32_t hpar_stamp = 0;
+    DevBuf hpar_count;                     // PARALLEL TransH: flagged samples of the last two batches
+    uint32_t hpar_orth_min = 0;            // ... from which normOrth takes the relation pass
     // PARALLEL schedule: per-event records in sorted order (kernels_transe.hpp EventRecs)
     DevBuf ev_iota, ev_slot_sorted, ev_inv, seg_row, ev_meta, ev_words;
     // PARALLEL TransR (kernels_transr_parallel.hpp)
@@ -1137,6 +1139,10 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     if (g.model == KB2E_TRANSH && g.schedule == KB2E_SCHEDULE_PARALLEL) {
         c->hpar_orth.alloc((size_t)((c->B + 511) / 512) * 512);  // whole 8-byte words past B stay zero
         memset_sync(c->hpar_orth.p, 0, c->hpar_orth.bytes);
+        c->hpar_count.alloc(2 * 4);
+        memset_sync(c->hpar_count.p, 0, c->hpar_count.bytes);
+        const char* om = getenv("KB2E_HPAR_ORTH_MIN");  // tests: 0 always, a large value never
+        c->hpar_orth_min = om ? (uint32_t)std::max(0, atoi(om)) : kOrthRelMin;
         c->hpar_tag.alloc((size_t)c->cfg.num_entities * 8);  // zeroed: stamp 0 is never a batch's
         c->rpar_St = 1 << 30;  // build_transr_tiles(c, false): relation segment ranges only
         c->rpar_ntiles.alloc((size_t)(nkeys + 1) * 4);

@@ -47,6 +47,11 @@ struct HParArgs {
     uint8_t* orth_mask;       // [B] violating (update, row) pairs of each sample, bits u * 3 + {r, h, t}
     unsigned long long* ent_tag;  // [ne] stamp << 32 | multi << 31 | relation of the entity's flagged pairs
     uint32_t stamp;           // this batch's tag stamp (never 0)
+    // normOrth's relation pass runs when the previous batch flagged >= orth_rel_min samples
+    // (few flagged pairs: the one-wave pass alone is cheaper); counts alternate by batch
+    uint32_t* orth_count_cur;   // this batch's flagged samples (check kernel)
+    uint32_t* orth_count_prev;  // the previous batch's (read by the relation pass, then zeroed)
+    uint32_t orth_rel_min;
 };
 
 // The flagged entity rows' relations this batch: the first relation a row is
@@ -203,6 +208,7 @@ __global__ __launch_bounds__(256) void transh_orth_check_kernel(HParArgs<T> a) {
     }
     if (l == 0) {
         a.orth_mask[kk] = (uint8_t)mask;
+        if (mask) atomicAdd(a.orth_count_cur, 1u);
         const int ids[6] = {r, h, t, r, nh, nt};
         for (int q = 1; q < 6; ++q)
             if (q != 3 && ((mask >> q) & 1u)) orth_tag_entity(a, ids[q], r);
@@ -218,6 +224,9 @@ __global__ __launch_bounds__(256) void transh_orth_check_kernel(HParArgs<T> a) {
 // relation (the reference reloads what it just stored), and a store is drained
 // only before a later load of the same row (PendingRows).
 constexpr int kOrthWords = 4;  // 8-byte flag words per lane per pass
+// flagged samples of the previous batch from which normOrth takes the relation pass
+// (KB2E_HPAR_ORTH_MIN; oracle/parallel.py ORTH_REL_MIN)
+constexpr uint32_t kOrthRelMin = 256;
 
 // Rows stored by this wave and not yet drained: a load of one of them waits
 // for the stores first (s_waitcnt vmcnt(0)); everything else loads at once.
@@ -320,6 +329,7 @@ __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
     }
     if (wid >= 0) row_store_sc1(W, a.w + (int64_t)wid * a.ld, a.n);
     drain_stores();
+    if (l == 0) *a.orth_count_prev = 0;  // read by this batch's relation pass; the next batch counts into it
 }
 
 // normOrth, first pass (oracle/parallel.py transh_parallel_batches): one wave per
@@ -330,6 +340,9 @@ __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
 // several relations flagged.  The relations' passes touch disjoint rows.
 template <typename T, int CH>
 __global__ __launch_bounds__(256) void transh_orth_rel_kernel(HParArgs<T> a) {
+    // few flagged pairs in the previous batch: leave every pair to the one-wave pass
+    // (the same rule in oracle/parallel.py transh_parallel_batches)
+    if (*a.orth_count_prev < a.orth_rel_min) return;
     const int s = a.rel_begin[a.batch] + (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
     if (s >= a.batch_seg[a.batch + 1]) return;
     const int l = lane_id();

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kWideThreads) void transr_cons_chain_wide_kernel(RP
     const bool colt = c < NP;             // (4 NP <= 512 threads)
     const T lr = (T)a.lr;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    T* Wc = (T*)smem;            // [NP][LW]
+    T* Wc = (T*)smem;            // [NP][LW] W'_r as the chain found it, then K0 = W'^T W' (the working matrix is in registers)
     T* A = Wc + NP * LW;         // [R][LW] the chunk's entity rows
     T* P = A + R * LW;           // [R][LW] projections; the violators' rows then hold G
     T* Gm = P + R * LW;          // [R][LG]
@@ -151,10 +151,18 @@ __global__ __launch_bounds__(kWideThreads) void transr_cons_chain_wide_kernel(RP
         const int j = idx / NP, i = idx % NP;
         Wc[j * LW + i] = (j < n && i < n) ? bf.W[((int64_t)r * n + j) * ld + i] : T(0);
     }
-    T k0[KQ];
-#pragma unroll
-    for (int i = 0; i < KQ; ++i) k0[i] = T(0);
     bool have_k0 = false, changed = false;
+    // The working matrix W_c in registers, as the MFMA B fragments of the projection
+    // tiles: wave w < NB, lane (kq, l16) holds W_c[4 s + kq][16 w + l16], s < NP / 4.
+    // The P tiles read no B operand from LDS, and a violator's W_c -= lr a^T g is
+    // register FMAs (its a and g rows broadcast from LDS) instead of an LDS
+    // read-modify-write of the whole matrix.
+    const bool wown = w < NB;
+    const int wcol = 16 * w + l16;
+    __syncthreads();  // (W' in LDS)
+    T bW[NP / 4];
+#pragma unroll
+    for (int q = 0; q < NP / 4; ++q) bW[q] = wown ? Wc[(4 * q + kq) * LW + wcol] : T(0);
     tick(0);
 
     // the chunk's rows: R x NP elements, RPT a thread, into registers (every load is
@@ -196,39 +204,22 @@ __global__ __launch_bounds__(kWideThreads) void transr_cons_chain_wide_kernel(RP
         __syncthreads();  // A (and W_c) ready
         if (nb < ne) load_rows(nb, ne);
         tick(2);
-        // P = A W_c (NB column tiles) and the Gram tile A A^T (its B operand is the A
-        // operand itself), a tile a wave; NP / 4 k-steps over the zero padding,
-        // straight-line, four k-steps' fragments a block
+        // P = A W_c (NB column tiles, B from the registers) and the Gram tile A A^T
+        // (its B operand is the A operand itself), a tile a wave, NP / 4 k-steps over
+        // the zero padding: straight-line code, no per-step guards
         if (w <= NB) {
             const bool gram = w == NB;
             const T* ap = A + l16 * LW + kq;
-            const T* bp = gram ? ap : Wc + kq * LW + w * 16 + l16;
-            const int bstep = gram ? 4 : 4 * LW;
             typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
-            // blocks of four k-steps, the next block's fragments loaded during this one's MFMAs
-            T av[4], bv[4];
+            T av[NP / 4];
 #pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                av[s4] = ap[4 * s4];
-                bv[s4] = bp[bstep * s4];
-            }
-#pragma unroll 1
-            for (int kb = 0; kb < NP / 4; kb += 4) {
-                T an[4], bn[4];
-                if (kb + 4 < NP / 4) {
+            for (int q = 0; q < NP / 4; ++q) av[q] = ap[4 * q];
+            if (gram) {
 #pragma unroll
-                    for (int s4 = 0; s4 < 4; ++s4) {
-                        an[s4] = ap[4 * (kb + 4 + s4)];
-                        bn[s4] = bp[bstep * (kb + 4 + s4)];
-                    }
-                }
+                for (int q = 0; q < NP / 4; ++q) acc = M::mma(av[q], av[q], acc);
+            } else {
 #pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4) acc = M::mma(av[s4], bv[s4], acc);
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4) {
-                    av[s4] = an[s4];
-                    bv[s4] = bn[s4];
-                }
+                for (int q = 0; q < NP / 4; ++q) acc = M::mma(av[q], bW[q], acc);
             }
             if (gram) {
 #pragma unroll
@@ -264,8 +255,11 @@ __global__ __launch_bounds__(kWideThreads) void transr_cons_chain_wide_kernel(RP
             tick(4);
             return;
         }
-        if (!have_k0) {  // K0[:, c] rows of quarter h = sum_j W[j][i] W[j][c] (W_c is still W'_r)
+        if (!have_k0) {  // K0 = W'^T W' in place of W' (LDS): thread (c, h) rows of quarter h of column c
             have_k0 = true;
+            T k0[KQ];
+#pragma unroll
+            for (int i = 0; i < KQ; ++i) k0[i] = T(0);
             if (colt) {
                 for (int jr = 0; jr < n; ++jr) {
                     const T wc = Wc[jr * LW + c];
@@ -278,6 +272,12 @@ __global__ __launch_bounds__(kWideThreads) void transr_cons_chain_wide_kernel(RP
                     }
                 }
             }
+            __syncthreads();  // every thread done with W'
+            if (colt) {
+#pragma unroll
+                for (int i = 0; i < KQ; ++i) Wc[(h * KQ + i) * LW + c] = k0[i];
+            }
+            __syncthreads();
         }
         tick(4);
         const T eps = T(2) * lr;
@@ -286,22 +286,28 @@ __global__ __launch_bounds__(kWideThreads) void transr_cons_chain_wide_kernel(RP
             cand &= ~((1u << cursor) - 1);
             if (!cand) break;
             const int v = __builtin_ctz(cand);
-            // V_c = sum_i p_v[i] K0[i][c], the quarters of the rows in the lanes of a quad
+            // V_c = sum_i p_v[i] K0[i][c] (K0 in LDS), the quarters of the rows in the lanes of a quad
             T V = T(0), pv = T(0);
             if (colt) {
                 T acc4[4] = {T(0), T(0), T(0), T(0)};
                 const double2* prow = (const double2*)(P + v * LW + h * KQ);
+                const T* kcol = Wc + h * KQ * LW + c;
                 pv = P[v * LW + c];
 #pragma unroll
-                for (int i0 = 0; i0 < KQ / 2; i0 += NB) {  // NB double2 loads in flight a block
+                for (int i0 = 0; i0 < KQ / 2; i0 += NB) {  // NB double2 + 2 NB K0 loads in flight a block
                     double2 pr[NB];
+                    T kk[2 * NB];
 #pragma unroll
-                    for (int i2 = 0; i2 < NB; ++i2) pr[i2] = prow[i0 + i2];
+                    for (int i2 = 0; i2 < NB; ++i2) {
+                        pr[i2] = prow[i0 + i2];
+                        kk[2 * i2] = kcol[(2 * (i0 + i2)) * LW];
+                        kk[2 * i2 + 1] = kcol[(2 * (i0 + i2) + 1) * LW];
+                    }
 #pragma unroll
                     for (int i2 = 0; i2 < NB; ++i2) {
                         const int i = 2 * (i0 + i2);
-                        acc4[i & 3] = fma(pr[i2].x, k0[i], acc4[i & 3]);
-                        acc4[(i + 1) & 3] = fma(pr[i2].y, k0[i + 1], acc4[(i + 1) & 3]);
+                        acc4[i & 3] = fma(pr[i2].x, kk[2 * i2], acc4[i & 3]);
+                        acc4[(i + 1) & 3] = fma(pr[i2].y, kk[2 * i2 + 1], acc4[(i + 1) & 3]);
                     }
                 }
                 V = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
@@ -389,25 +395,13 @@ __global__ __launch_bounds__(kWideThreads) void transr_cons_chain_wide_kernel(RP
                 if (sl < 0) bf.relpair_stamp[r] = bf.stamp;
             }
         }
-        if (colt && c < n) {  // rows of quarter h of column c (this thread's alone), four at a time in registers
+        if (wown) {  // W_c[4 s + kq][wcol] -= lr a_v[4 s + kq] g_v[wcol], in the fragments
+            for (uint32_t mm = vmask; mm; mm &= mm - 1) {
+                const int v = __builtin_ctz(mm);
+                const T gl = -lr * P[v * LW + wcol];
+                const T* av = A + v * LW + kq;
 #pragma unroll
-            for (int k0r = 0; k0r < KQ; k0r += 4) {
-                const int k = h * KQ + k0r;
-                T wv[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) wv[u] = Wc[(k + u) * LW + c];
-                for (uint32_t mm = vmask; mm; mm &= mm - 1) {
-                    const int v = __builtin_ctz(mm);
-                    const T gl = -lr * P[v * LW + c];
-                    const double2* ar = (const double2*)(A + v * LW + k);
-                    const double2 a0 = ar[0], a1 = ar[1];
-                    wv[0] = fma(a0.x, gl, wv[0]);
-                    wv[1] = fma(a0.y, gl, wv[1]);
-                    wv[2] = fma(a1.x, gl, wv[2]);
-                    wv[3] = fma(a1.y, gl, wv[3]);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) Wc[(k + u) * LW + c] = wv[u];
+                for (int q = 0; q < NP / 4; ++q) bW[q] = fma(av[4 * q], gl, bW[q]);
             }
         }
         tick(11);
@@ -520,14 +514,26 @@ __global__ __launch_bounds__(kWideThreads) void transr_cons_chain_wide_kernel(RP
         }
     }
     if (ntail > 0) {
-        if (changed) {  // the last update's unit rows (transr/trainer.cpp:178-180): row c, quarter h of the columns
-            const int jr = c;
-            T sq = T(0);
-            if (colt && jr < n)
-                for (int i = h * KQ; i < min(n, (h + 1) * KQ); ++i) sq = fma(Wc[jr * LW + i], Wc[jr * LW + i], sq);
-            const T len = sqrt(quad_sum(sq));
-            if (colt && jr < n)
-                for (int i = h * KQ; i < min(n, (h + 1) * KQ); ++i) Wc[jr * LW + i] = Wc[jr * LW + i] / len;
+        if (changed) {  // the last update's unit rows (transr/trainer.cpp:178-180)
+            // row 4 s + kq: its 16 columns of tile w summed in the DPP row, the tiles in
+            // LDS (qpart's and red's space is free here: P [R][LW] >= NB x NP)
+            T* rs = P;  // [NB][NP] row partials
+#pragma unroll
+            for (int q = 0; q < NP / 4; ++q) {
+                T x[1] = {bW[q] * bW[q]};
+                row16_sums<T, 1>(x);
+                if (wown && l16 == 0) rs[w * NP + 4 * q + kq] = x[0];
+            }
+            __syncthreads();
+            if (wown) {
+#pragma unroll
+                for (int q = 0; q < NP / 4; ++q) {
+                    const int jr = 4 * q + kq;
+                    T ss = rs[jr];
+                    for (int v = 1; v < NB; ++v) ss += rs[v * NP + jr];
+                    if (jr < n) bW[q] = bW[q] / sqrt(ss);
+                }
+            }
         }
         __syncthreads();  // the tail list and W_c
         load_rows(0, ntail);
@@ -539,10 +545,11 @@ __global__ __launch_bounds__(kWideThreads) void transr_cons_chain_wide_kernel(RP
         for (int k = 0; k < 2; ++k) bf.pflag[kl * 4 + 2 + k] = ((tkeep >> k) & 1) ? vflag[pos++] : 0;
     }
     tick(14);
-    // the relation's matrix back
-    for (int idx = tid; idx < n * n; idx += NT) {
-        const int j = idx / n, i = idx % n;
-        bf.W[((int64_t)r * n + j) * ld + i] = Wc[j * LW + i];
+    // the relation's matrix back, from the fragments
+    if (wown && wcol < n) {
+#pragma unroll
+        for (int q = 0; q < NP / 4; ++q)
+            if (4 * q + kq < n) bf.W[((int64_t)r * n + 4 * q + kq) * ld + wcol] = bW[q];
     }
     if (bf.stats && tid == 0) {
         const unsigned long long cyc = (unsigned long long)(clock64() - ck0);

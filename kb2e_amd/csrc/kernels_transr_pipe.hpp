@@ -12,8 +12,14 @@
 //   X_{k+1} = A_{k+1} W_{k-1}                  (the matrix before chunk k's walk)
 //   C       = A_{k+1} A_k^T                    (cross Gram, next x current)
 //   P_{k+1} = X_{k+1} - lr C[:, vio_k] G_k     (chunk k's shrinks, W_k = W_{k-1} - lr A_k^T G_k)
-// so after the walk only a rank-|vio_k| correction, the W update and the next
-// chunk's |p|^2 sit between two walks.  The walk keeps the chunk's projection
+// so after the walk only a rank-|vio_k| correction and the next chunk's |p|^2
+// sit between two walks.  The working matrix W_c lives in registers of waves
+// 1-3 as the MFMA B fragments of their column slices (slice cb on wave
+// 1 + cb % 3), so X's tiles read no B operand from LDS, and chunk k's update
+// W_c -= lr A_k^T G_k and its pair records are made by waves 1-3 at the start of
+// chunk k+1, while wave 0 walks chunk k+1, instead of between the two walks (a
+// wave touches only its own slices' columns of the P buffers, so reading G_k
+// and writing X_{k+2} into the same buffer need no barrier).  The walk keeps the chunk's projection
 // rows in registers (lane j: half l >> 5 of row j & 31), so a violator's
 // rank-1 move of the later rows is FMAs on registers with the violator's G row
 // read as LDS broadcasts.  The relation's last-update chunk starts after W_c's
@@ -27,15 +33,16 @@ namespace kb2e {
 
 constexpr int kPipeList = 1536;  // pairs of one relation a window (entity and slot lists in LDS)
 
-// LDS (elements of T): W_c [NP][L] | A [3][R][L] | P [2][R][L] (K0 [NP][L] in the
-// prologue) | Gram [2][R][LG] | cross Gram [R][LG] | |p|^2 partials [4][R] | row
-// partials [4][NP]; ints: pair entities, slots [kPipeList] each | pre
-// [kSeqMaxTiles + 1] | misc [8] | the chunk's violators [R]
+// LDS (elements of T): W_c [NP][L] (W' for K0; the final matrix for the records) |
+// A [3][R][L] | P [2][R][L] (K0 [NP][L] in the prologue) | Gram [2][R][LG] | cross
+// Gram [R][LG] | |p|^2 partials [4][R] | row partials [4][NP]; ints: pair entities,
+// slots [kPipeList] each | pre [kSeqMaxTiles + 1] | misc [8] | the violators of the
+// last two chunks [2][R]
 template <typename T>
 __host__ __device__ constexpr size_t pipe_lds(int n) {
     return sizeof(T) * ((size_t)rm_np(n) * rm_ld(n) + 5 * (size_t)kChainRows * rm_ld(n) +
                         3 * (size_t)kChainRows * (kChainRows + 1) + 4 * kChainRows + 4 * (size_t)rm_np(n)) +
-           sizeof(int) * (size_t)(2 * kPipeList + kSeqMaxTiles + 1 + 8 + kChainRows);
+           sizeof(int) * (size_t)(2 * kPipeList + kSeqMaxTiles + 1 + 8 + 2 * kChainRows);
 }
 
 template <typename T, int KS>
@@ -45,14 +52,17 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
     constexpr int NB = (4 * KS + 15) / 16;  // column slices of 16
     constexpr int NP = 16 * NB, L = NP + 2, R = kChainRows, LG = R + 1;
     constexpr int NH = NP / 2;              // columns of a row half (walk registers)
+    constexpr int NSW = (NB + 2) / 3;       // column slices a helper wave owns (slice cb: wave 1 + cb % 3)
     static_assert(2 * R * L >= NP * L, "the K0 image borrows the two P buffers");
+    static_assert(NSW * KS <= 4 * KS, "the helpers' slices share the walk's K0 registers");
     const int t0 = a.batch_t0[a.batch], t1 = a.batch_t0[a.batch + 1];
     int g0, r;  // the relation's first tile within the batch
     if (!chain_first_tile(a, t0, t1, g0, r)) return;
     const int n = a.n, ld = a.ld;
     const int w = threadIdx.x >> 6, l = lane_id(), kq = l >> 4, l16 = l & 15;
-    const bool mine = w < NB;  // this wave owns a column slice (K0, the W_c update)
+    const bool mine = w < NB;  // this wave computes a column slice of K0
     const int col = 16 * w + l16;
+    const int hw = w - 1;      // helper wave index (waves 1-3)
     const T lr = (T)a.lr;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* Wc = (T*)smem;
@@ -66,10 +76,11 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
     int* ps = pe + kPipeList;
     int* pre = ps + kPipeList;
     int* misc = pre + kSeqMaxTiles + 1;
-    int* vlist = misc + 8;  // the current chunk's violators in order (misc[2]: their count)
+    int* vlist = misc + 8;  // [2][R] the chunks' violators in order, by chunk parity (misc[2]: the count)
     const long long ck0 = clock64();
     unsigned long long n_chunks = 0, n_vio = 0, n_rounds = 0, max_m = 0;
-    unsigned long long ph[16] = {};
+    __shared__ unsigned long long ph[16];  // (LDS, not sixteen 64-bit registers)
+    if (threadIdx.x < 16) ph[threadIdx.x] = 0;
     long long tq = ck0;
     auto tick = [&](int k) {
         if (bf.stats && threadIdx.x == 0) {
@@ -122,8 +133,9 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
     }
     __syncthreads();
     const int run = misc[5], has_rel = misc[3], g_tail = misc[4], n_tail = misc[6];
-    // K0 = W'^T W' (four waves, MFMA) into the P buffers, wave 0 keeps column l
-    T k0c[4 * KS];
+    // K0 = W'^T W' (four waves, MFMA) into the P buffers; wave 0 keeps column l of it,
+    // the helper waves their slices of W' (the working matrix) -- in the same registers
+    T reg[4 * KS];
     {
         T* K0 = Pbuf;
         if (mine) {
@@ -146,29 +158,54 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
         if (w == 0) {
             const int cK = l < NP ? l : 0;
 #pragma unroll
-            for (int i = 0; i < 4 * KS; ++i) k0c[i] = K0[i * L + cK];
+            for (int i = 0; i < 4 * KS; ++i) reg[i] = K0[i * L + cK];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4 * KS; ++i) reg[i] = T(0);
+#pragma unroll
+            for (int si = 0; si < NSW; ++si) {
+                const int cb = hw + 3 * si;
+                if (cb < NB) {
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) reg[si * KS + s] = Wc[(4 * s + kq) * L + cb * 16 + l16];
+                }
+            }
         }
         __syncthreads();  // the P buffers are free again
     }
     bool changed = false;
     int32_t* const vio = bf.vio + (int64_t)g0 * kCPairs;  // the relation's violators (run * kCPairs >= its pairs)
     int nvt = 0;
+    // the chunk whose W_c update and pair records the helper waves still owe (nv 0: none)
+    int pend_nv = 0, pend_par = 0, pend_pc = 0, pend_ka = 0, pend_base = 0, pend_nvt = 0;
     tick(0);
 
-    // one 16 x 16 MFMA tile: rows rt of A (Ar) against Wc columns cb (gram = false)
-    // or against rows cb of B (gram = true); out[(rt 16 + d) * ldo + cb 16 + l16]
-    auto mfma_tile = [&](const T* Ar, const T* Bm, bool gram, int rt, int cb, T* out, int ldo) {
+    // one 16 x 16 MFMA tile: rows rt of A (Ar) against rows cb of B (a Gram tile);
+    // out[(rt 16 + d) * ldo + cb 16 + l16]
+    auto gram_tile = [&](const T* Ar, const T* Bm, int rt, int cb, T* out, int ldo) {
         typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
         T av[KS], bv[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             av[s] = Ar[(rt * 16 + l16) * L + 4 * s + kq];
-            bv[s] = gram ? Bm[(cb * 16 + l16) * L + 4 * s + kq] : Wc[(4 * s + kq) * L + cb * 16 + l16];
+            bv[s] = Bm[(cb * 16 + l16) * L + 4 * s + kq];
         }
 #pragma unroll
         for (int s = 0; s < KS; ++s) acc = M::mma(av[s], bv[s], acc);
 #pragma unroll
         for (int q = 0; q < 4; ++q) out[(rt * 16 + kq + 4 * q) * ldo + cb * 16 + l16] = acc[q];
+    };
+    // rows rt of A against the helper's column slice si (its W_c fragments)
+    auto proj_tile = [&](const T* Ar, int rt, int si, T* out) {
+        const int cb = hw + 3 * si;
+        typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
+        T av[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) av[s] = Ar[(rt * 16 + l16) * L + 4 * s + kq];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) acc = M::mma(av[s], reg[si * KS + s], acc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[(rt * 16 + kq + 4 * q) * L + cb * 16 + l16] = acc[q];
     };
     // rows of chunk [b, e) of the window: R NP / 256 elements a thread, in registers
     constexpr int kRowsPer = R * NP / kChainThreads;
@@ -198,11 +235,11 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
             Abuf[slot * R * L + (idx / NP) * L + idx % NP] = ((rows_ok >> q) & 1) ? rows[q] : T(0);
         }
     };
-    // P_n -= lr C[:, vio] G over the chunk's nv violators (vlist; G: their rows of
+    // P_n -= lr C[:, vio] G over the chunk's nv violators (vl; G: their rows of
     // Pc) and the |p_j|^2 partials of the cn rows (qpart[0]; the other slices'
     // partials zero), eight threads a row, NP / 8 columns each (on the VALU: the
     // few violators of a chunk make an MFMA form latency-bound)
-    auto correct_q = [&](T* Pn, int cn, int nv, const T* Pc) {
+    auto correct_q = [&](T* Pn, int cn, int nv, const T* Pc, const int* vl) {
         constexpr int NE = NP / 8;
         const int j = threadIdx.x >> 3, cb = (threadIdx.x & 7) * NE;
         T sq = T(0);
@@ -211,7 +248,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
 #pragma unroll
             for (int u = 0; u < NE; ++u) x[u] = Pn[j * L + cb + u];
             for (int k = 0; k < nv; ++k) {
-                const int v = vlist[k];
+                const int v = vl[k];
                 const T gl = -lr * Cx[j * LG + v];
 #pragma unroll
                 for (int u = 0; u < NE; ++u) x[u] = fma(gl, Pc[v * L + cb + u], x[u]);
@@ -230,39 +267,80 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
             for (int v = 1; v < NB; ++v) qpart[v * R + j] = T(0);
         }
     };
-    // the relation's last update renormalises W_c's rows before its own pairs'
-    // shrinks (transr/trainer.cpp:178-180); ends with a barrier
-    auto renorm = [&] {
-        if (mine && l < NP) {
-            T sq = T(0);
-            if (l < n)
-                for (int i = 0; i < 16; ++i) sq += Wc[l * L + 16 * w + i] * Wc[l * L + 16 * w + i];
-            rp[w * NP + l] = sq;
+    // the helper waves' debt: the pending chunk's W_c -= lr A^T G on their slices
+    // (its G rows in P buffer pend_pc, its rows in A slot pend_ka) and its pair records
+    // (each wave its own slices' columns; lanes of DPP row kq take violators kq, kq + 4, ...)
+    auto apply_pending = [&]() {
+        if (w == 0 || pend_nv == 0) return;
+        const T* Pp = Pbuf + pend_pc * R * L;
+        const T* Ap = Abuf + pend_ka * R * L;
+        const int* vl = vlist + pend_par * R;
+#pragma unroll
+        for (int si = 0; si < NSW; ++si) {
+            const int cb = hw + 3 * si;
+            if (cb >= NB) continue;
+            const int c = cb * 16 + l16;
+            for (int k = 0; k < pend_nv; ++k) {
+                const int v = vl[k];
+                const T gl = -lr * Pp[v * L + c];
+#pragma unroll
+                for (int s = 0; s < KS; ++s) reg[si * KS + s] = fma(Ap[v * L + 4 * s + kq], gl, reg[si * KS + s]);
+            }
+            for (int k = kq; k < pend_nv; k += 4) {
+                const int v = vl[k];
+                const int sl = ps[pend_base + v];
+                T* dst = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
+                if (c < n) dst[c] = Pp[v * L + c];
+                if (hw == 0 && si == 0 && l16 == 0) vio[pend_nvt + k] = sl;
+            }
         }
-        __syncthreads();
-        if (mine && l < n) {
-            T ss = rp[l];
-            for (int v = 1; v < NB; ++v) ss += rp[v * NP + l];
-            const T len = sqrt(ss);
-            for (int i = 0; i < 16; ++i) Wc[l * L + 16 * w + i] = Wc[l * L + 16 * w + i] / len;
-        }
-        __syncthreads();
     };
-    // projections and Gram matrix of a chunk afresh, all four waves, then the |p|^2
-    // partials (two barriers; the chunk's rows are in LDS)
-    auto fresh = [&](const T* A, int cc, T* P, T* G) {
-        const int nrt = cc > 16 ? 2 : 1;
-        const int ntiles = nrt * NB + (nrt == 2 ? 3 : 1);
-        for (int tl = w; tl < ntiles; tl += kChainThreads / kWave) {
-            if (tl < nrt * NB) {
-                mfma_tile(A, nullptr, false, tl / NB, tl % NB, P, L);
-            } else {
-                const int gi = tl - nrt * NB;
-                mfma_tile(A, A, true, gi == 0 ? 0 : 1, gi == 2 ? 1 : 0, G, LG);
+    // the relation's last update renormalises W_c's rows before its own pairs'
+    // shrinks (transr/trainer.cpp:178-180): row sums of the slices in DPP rows, then
+    // LDS; ends with a barrier.  The pending update must be applied first.
+    auto renorm = [&] {
+        if (w > 0) {
+#pragma unroll
+            for (int si = 0; si < NSW; ++si) {
+                const int cb = hw + 3 * si;
+#pragma unroll
+                for (int s = 0; s < KS; ++s) {
+                    T x[1] = {reg[si * KS + s] * reg[si * KS + s]};
+                    row16_sums<T, 1>(x);
+                    if (cb < NB && l16 == 0) rp[cb * NP + 4 * s + kq] = x[0];
+                }
             }
         }
         __syncthreads();
-        correct_q(P, cc, 0, nullptr);
+        if (w > 0) {
+#pragma unroll
+            for (int si = 0; si < NSW; ++si) {
+                if (hw + 3 * si >= NB) continue;
+#pragma unroll
+                for (int s = 0; s < KS; ++s) {
+                    const int jr = 4 * s + kq;
+                    T ss = rp[jr];
+                    for (int v = 1; v < NB; ++v) ss += rp[v * NP + jr];
+                    if (jr < n) reg[si * KS + s] = reg[si * KS + s] / sqrt(ss);
+                }
+            }
+        }
+        __syncthreads();
+    };
+    // projections and Gram matrix of a chunk afresh (the helpers their slices, wave 0
+    // the Gram tiles), then the |p|^2 partials (two barriers; the chunk's rows in LDS)
+    auto fresh = [&](const T* A, int cc, T* P, T* G) {
+        const int nrt = cc > 16 ? 2 : 1;
+        if (w > 0) {
+#pragma unroll
+            for (int si = 0; si < NSW; ++si)
+                if (hw + 3 * si < NB)
+                    for (int rt = 0; rt < nrt; ++rt) proj_tile(A, rt, si, P);
+        } else {
+            for (int gi = 0; gi < (nrt == 2 ? 3 : 1); ++gi) gram_tile(A, A, gi == 0 ? 0 : 1, gi == 2 ? 1 : 0, G, LG);
+        }
+        __syncthreads();
+        correct_q(P, cc, 0, nullptr, vlist);
         __syncthreads();
     };
 
@@ -273,6 +351,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
     const int tile_cap = bf.chain_tiles >= 1 && bf.chain_tiles < kSeqMaxTiles ? bf.chain_tiles : kSeqMaxTiles;
     const int list_cap = bf.chain_list >= 64 && bf.chain_list < kPipeList ? bf.chain_list : kPipeList;
     int pc = 0;  // P / Gram buffer of the current chunk
+    int par = 0;  // vlist parity of the current chunk
     for (int gw = g0; gw < g0 + run || gw == g0;) {
         if (w == 0) {  // exclusive prefix of the window's tile pair counts (the relation pair left out)
             const int nt = g0 + run - gw < tile_cap ? g0 + run - gw : tile_cap;
@@ -353,6 +432,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
             T* Pn = Pbuf + (pc ^ 1) * R * L;
             T* Gm = Gbuf + pc * R * LG;
             T* Gn = Gbuf + (pc ^ 1) * R * LG;
+            int* vl = vlist + par * R;
             ++n_chunks;
             tick(1);
             if (w == 0) {
@@ -389,7 +469,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
 #pragma unroll
                         for (int t = 0; t < KS; ++t)
 #pragma unroll
-                            for (int u = 0; u < 4; ++u) vv4[u] = fma(P[v * L + 4 * t + u], k0c[4 * t + u], vv4[u]);
+                            for (int u = 0; u < 4; ++u) vv4[u] = fma(P[v * L + 4 * t + u], reg[4 * t + u], vv4[u]);
                         const T Vc = c < n ? (vv4[0] + vv4[1]) + (vv4[2] + vv4[3]) : T(0);
                         tick(7);
                         T s2[2] = {pv * Vc, Vc * Vc};
@@ -435,31 +515,31 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                 }
                 if (l < cc) {  // the chunk's pair flags; (entity'[r], r) marks the relation
                     const int sl = ps[base + l];
-                    const bool vio = (vmask >> l) & 1;
-                    if (sl >= 0) bf.pflag[sl] = vio ? 1 : 0;
-                    else if (vio) bf.relpair_stamp[r] = bf.stamp;
+                    const bool vio_l = (vmask >> l) & 1;
+                    if (sl >= 0) bf.pflag[sl] = vio_l ? 1 : 0;
+                    else if (vio_l) bf.relpair_stamp[r] = bf.stamp;
                 }
-                if (l < R && ((vmask >> l) & 1u)) vlist[__builtin_popcount(vmask & ((1u << l) - 1u))] = l;
+                if (l < R && ((vmask >> l) & 1u)) vl[__builtin_popcount(vmask & ((1u << l) - 1u))] = l;
                 if (l == 0) {
                     misc[1] = (int)vmask;
                     misc[2] = __builtin_popcount(vmask);
                 }
                 tick(2);
-            } else if (cn > 0) {
-                // the next chunk against W_{k-1}: X = A_{k+1} W_c, its Gram matrix, and the
-                // cross Gram A_{k+1} A_k^T, 16 x 16 tiles dealt round waves 1-3
-                const int nrt = cn > 16 ? 2 : 1, crt = cc > 16 ? 2 : 1;
-                const int nx = nrt * NB, ng = nrt == 2 ? 3 : 1;
-                const int ntiles = nx + ng + nrt * crt;
-                for (int tl = w - 1; tl < ntiles; tl += kChainThreads / kWave - 1) {
-                    if (tl < nx) {
-                        mfma_tile(An, nullptr, false, tl / NB, tl % NB, Pn, L);
-                    } else if (tl < nx + ng) {
-                        const int gi = tl - nx;
-                        mfma_tile(An, An, true, gi == 0 ? 0 : 1, gi == 2 ? 1 : 0, Gn, LG);
-                    } else {
-                        const int ci = tl - nx - ng;
-                        mfma_tile(An, A, true, ci / crt, ci % crt, Cx, LG);
+            } else {
+                // chunk k-1's W_c update and records, then the next chunk against W_{k-1}:
+                // X = A_{k+1} W_c (each helper its own slices), its Gram matrix and the cross
+                // Gram A_{k+1} A_k^T (waves 2 and 3)
+                apply_pending();
+                if (cn > 0) {
+                    const int nrt = cn > 16 ? 2 : 1, crt = cc > 16 ? 2 : 1;
+#pragma unroll
+                    for (int si = 0; si < NSW; ++si)
+                        if (hw + 3 * si < NB)
+                            for (int rt = 0; rt < nrt; ++rt) proj_tile(An, rt, si, Pn);
+                    const int ng = nrt == 2 ? 3 : 1;
+                    for (int tl = hw; tl < ng + nrt * crt; tl += 3) {
+                        if (tl < ng) gram_tile(An, An, tl == 0 ? 0 : 1, tl == 2 ? 1 : 0, Gn, LG);
+                        else gram_tile(An, A, (tl - ng) / crt, (tl - ng) % crt, Cx, LG);
                     }
                 }
             }
@@ -467,8 +547,17 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
             tick(3);
             const uint32_t vmask = (uint32_t)misc[1];
             const int nv = misc[2];
-            // chunk k+2's rows into the slot chunk k - 1 left, chunk k+3's in flight
-            // (first: the wait for the rows loaded a chunk ago then covers no store)
+            // chunk k's debt passes to the helpers (paid at the next chunk, or below)
+            pend_nv = nv;
+            pend_par = par;
+            pend_pc = pc;
+            pend_ka = ka;
+            pend_base = base;
+            pend_nvt = nvt;
+            nvt += nv;
+            if (vmask) changed = true;
+            // chunk k+2's rows into the slot chunk k - 1 left (its debt is paid), chunk
+            // k+3's in flight
             const int ka2 = ka == 0 ? 2 : ka - 1;
             if (nb2 < npairs || cn > 0) {
                 store_rows(ka2);
@@ -476,55 +565,44 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                 load_rows(n3, n3 < npairs ? chunk_end(n3) : n3);
             }
             tick(12);
-            if (vmask) {
-                changed = true;
-                // W_c[:, slice] -= lr sum_v A[v]^T G[v] over the chunk's violators
-                if (mine) {
-                    T wv[KS];
-#pragma unroll
-                    for (int t = 0; t < KS; ++t) wv[t] = Wc[(kq + 4 * t) * L + col];
-                    for (int k = 0; k < nv; ++k) {
-                        const int v = vlist[k];
-                        const T gl = -lr * P[v * L + col];
-#pragma unroll
-                        for (int t = 0; t < KS; ++t) wv[t] = fma(A[v * L + kq + 4 * t], gl, wv[t]);
-                    }
-#pragma unroll
-                    for (int t = 0; t < KS; ++t) Wc[(kq + 4 * t) * L + col] = wv[t];
-                }
-            }
-            tick(13);
             const bool restart = nbase == tail_start && changed && cn > 0;  // the tail: afresh
-            if (cn > 0 && !restart) correct_q(Pn, cn, nv, P);
+            if (cn > 0 && !restart) correct_q(Pn, cn, nv, P, vl);
             tick(14);
-            if (vmask) {  // the violators' pair records G (da = -lr W G at the end), a wave each
-                for (int k = w; k < nv; k += kChainThreads / kWave) {
-                    const int v = vlist[k];
-                    const int sl = ps[base + v];
-                    T* dst = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
-                    if (l < n) dst[l] = P[v * L + l];
-                    if (l == 0) vio[nvt + k] = sl;
-                }
-                nvt += nv;
-            }
-            tick(15);
             __syncthreads();  // B2
             tick(6);
             if (restart) {
+                apply_pending();  // the matrix up to date before the rows' renorm
+                pend_nv = 0;
+                __syncthreads();
                 renorm();
                 fresh(An, cn, Pn, Gn);
             }
             pc ^= 1;
+            par ^= 1;
             ka = ka == 2 ? 0 : ka + 1;
             base = nbase;
         }
+        // the window's last debt before its lists are rebuilt
+        apply_pending();
+        pend_nv = 0;
+        __syncthreads();
         gw += ntile;
         if (last || gw >= g0 + run) break;
     }
-    // the relation's matrix back: each wave its column slice
+    // the relation's matrix back: the helpers' slices into LDS (the records' matrix), then HBM
+    if (w > 0) {
+#pragma unroll
+        for (int si = 0; si < NSW; ++si) {
+            const int cb = hw + 3 * si;
+            if (cb < NB) {
+#pragma unroll
+                for (int s = 0; s < KS; ++s) Wc[(4 * s + kq) * L + cb * 16 + l16] = reg[si * KS + s];
+            }
+        }
+    }
+    __syncthreads();
     if (mine && col < n)
         for (int jj = 0; jj < n; ++jj) bf.W[((int64_t)r * n + jj) * ld + col] = Wc[jj * L + col];
-    __syncthreads();  // (the last records written; the P buffers free)
     chain_records<T, NP, L>(a, bf, r, vio, nvt, Wc, Pbuf);
     if (bf.stats) {
         if (threadIdx.x == 0) {

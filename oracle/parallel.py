@@ -361,7 +361,11 @@ def transh_orth_order(samples, flags, ids, r):
     return out
 
 
-def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, rate, margin=1.0):
+ORTH_REL_MIN = 256  # kernels_transh_parallel.hpp kOrthRelMin
+
+
+def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, rate, margin=1.0, state=None,
+                            orth_rel_min=ORTH_REL_MIN):
     """Train `nbatches` TransH batches of the PARALLEL schedule in place
     (kb2e_amd/csrc/kernels_transh_parallel.hpp).  Returns (loss, active).
 
@@ -373,10 +377,15 @@ def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
     relation row once per sample) runs the reference's normOrth
     (common/utils.cpp:79-111): first the pairs whose row only their relation
     touches (per relation, samples in order), then the entity rows flagged
-    under several relations (samples in order).
+    under several relations (samples in order) -- when the previous batch
+    flagged at least `orth_rel_min` samples; otherwise every flagged pair in
+    sample order (the GPU's one-wave pass alone).  `state` carries the previous
+    batch's flagged-sample count across calls (the engine's, across epochs;
+    zero before the first batch).
     """
     from oracle import orc
 
+    state = {} if state is None else state
     loss = 0.0
     active = 0
     h_all, t_all, r_all = triples[:, 0], triples[:, 1], triples[:, 2]
@@ -426,7 +435,12 @@ def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
             rows = [(rel, r[kk]), (ent, h[kk]), (ent, t[kk]), None, (ent, nh[kk]), (ent, nt[kk])]
             flags.append([q for q in range(6) if rows[q] is not None and W[r[kk]] @ rows[q][0][rows[q][1]] > 0.1])
         ids = {kk: (r[kk], h[kk], t[kk], None, nh[kk], nt[kk]) for kk in a}
-        for kk, q in transh_orth_order(list(a), flags, ids, r):
+        if state.get("orth_flagged", 0) >= orth_rel_min:
+            order = transh_orth_order(list(a), flags, ids, r)
+        else:
+            order = [(kk, q) for kk, fl in zip(a, flags) for q in fl]
+        state["orth_flagged"] = sum(1 for fl in flags if fl)
+        for kk, q in order:
             rows = [(rel, r[kk]), (ent, h[kk]), (ent, t[kk]), None, (ent, nh[kk]), (ent, nt[kk])]
             tab, row = rows[q]
             va, vb = orc.norm_orth(tab[row], W[r[kk]], rate)

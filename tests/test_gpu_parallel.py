@@ -262,8 +262,8 @@ def test_transr_parallel_fp32_close(monkeypatch):
         assert abs(a64 - a32) <= 0.01 * a64 and abs(l64 - l32) <= 0.01 * l64
 
 
-def _transh_vs_model(ds, dim, epochs, *, batches=10, rate=0.01, seed=3, method=1, atol=1e-9):
-    from oracle.parallel import transh_parallel_batches
+def _transh_vs_model(ds, dim, epochs, *, batches=10, rate=0.01, seed=3, method=1, atol=1e-9, orth_min=None):
+    from oracle.parallel import ORTH_REL_MIN, transh_parallel_batches
     m = orc.Model("H", dim, ds.num_entities, ds.num_relations, rate=rate, method=method, batches=batches)
     m.set_triples(ds.train)
     orc.srand(seed)
@@ -275,9 +275,11 @@ def _transh_vs_model(ds, dim, epochs, *, batches=10, rate=0.01, seed=3, method=1
     e0, r0, w0 = eng.init_params()
     assert np.array_equal(e0, pe) and np.array_equal(r0, pr) and np.array_equal(w0, pw)
     B = m.batch_size()
+    state = {}  # the previous batch's flagged samples, across epochs as in the engine
     for ep in range(epochs):
         si, sj, side = m.sample_stream(B * batches)
-        lo, ao = transh_parallel_batches(pe, pr, pw, ds.train, si, sj, side, B, batches, rate=rate)
+        lo, ao = transh_parallel_batches(pe, pr, pw, ds.train, si, sj, side, B, batches, rate=rate, state=state,
+                                         orth_rel_min=ORTH_REL_MIN if orth_min is None else orth_min)
         lg, ag = eng.train_epoch()
         assert ag == ao, (ep, ag, ao)
         assert abs(lg - lo) <= 1e-9 * max(1.0, abs(lo))
@@ -290,6 +292,16 @@ def _transh_vs_model(ds, dim, epochs, *, batches=10, rate=0.01, seed=3, method=1
 def test_transh_parallel(dim):
     """Tiny set, lr 0.01: the orthogonality loop fires; ragged and multi-chunk widths."""
     _transh_vs_model(tiny(), dim, 2)
+
+
+@pytest.mark.parametrize("orth_min", [0, 1 << 30, 8])
+def test_transh_parallel_orth_gate(orth_min, monkeypatch):
+    """normOrth's relation pass runs only when the previous batch flagged at least
+    KB2E_HPAR_ORTH_MIN samples (0: always; huge: never, every pair on the one-wave
+    pass in sample order; 8: batches of both kinds on the tiny set); the CPU
+    model applies the same rule."""
+    monkeypatch.setenv("KB2E_HPAR_ORTH_MIN", str(orth_min))
+    _transh_vs_model(tiny(), 20, 2, orth_min=orth_min)
 
 
 def test_transh_parallel_small():

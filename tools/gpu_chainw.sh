@@ -7,7 +7,7 @@ set -o pipefail
 OUT=gpurun_out/${1:-chainw}
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 700 python -u -m pytest tests/test_gpu_parallel.py -x -v --timeout 300 --timeout-method thread -k "transr" > $OUT/par.log 2>&1 || { echo "parallel tests failed $?"; grep -E "^FAILED|Error|assert" $OUT/par.log | head -20; tail -5 $OUT/par.log; exit 1; }
+timeout -k 10 700 python -u -m pytest tests/test_gpu_parallel.py -x -v --timeout 300 --timeout-method thread -k "transr or transh" > $OUT/par.log 2>&1 || { echo "parallel tests failed $?"; grep -E "^FAILED|Error|assert" $OUT/par.log | head -20; tail -5 $OUT/par.log; exit 1; }
 tail -1 $OUT/par.log
 timeout -k 10 500 python -u -m pytest tests/test_gpu_k5.py tests/test_gpu_eval.py -x -v --timeout 400 --timeout-method thread > $OUT/k5.log 2>&1 || { echo "k5/eval tests failed $?"; grep -E "^FAILED|Error|assert" $OUT/k5.log | head -20; tail -5 $OUT/k5.log; exit 1; }
 tail -1 $OUT/k5.log
