@@ -159,7 +159,7 @@ struct kb2e_ctx {
     // PARALLEL schedule: per-event records in sorted order (kernels_transe.hpp EventRecs)
     DevBuf ev_iota, ev_slot_sorted, ev_inv, seg_row, ev_meta, ev_words;
     // PARALLEL TransR (kernels_transr_parallel.hpp)
-    int32_t rpar_St = 8, rpar_max_tiles = 1, rpar_tile_threads = 256;
+    int32_t rpar_St = 8, rpar_max_tiles = 1, rpar_tile_threads = 256, rpar_tgroup = 1;
     bool rpar_no_constraint = false;
     bool rpar_mfma = false;  // matrix-core tile kernels (kernels_transr_mfma.hpp)
     bool rpar_cons_wave = false;  // transRNorm rounds in one wave's registers (kernels_transr_cons.hpp)

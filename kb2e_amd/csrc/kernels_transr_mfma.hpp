@@ -176,13 +176,24 @@ __device__ __forceinline__ void matvec_t(const T* WT, int L, int n, const T* xl,
 
 // Tile: phase A (projections, energies / compat projections, x, d, y = W x) and
 // the gradient partials dW = D^T X, dr, as transr_tile_kernel.
+// Tile groups (a.tgroup > 1, eight-wave blocks): the block of a relation's tile
+// q = 0 (mod tgroup) runs tiles q .. q + tgroup - 1 of that relation one after
+// another -- W staged once, dW accumulated in the waves' MFMA registers -- and
+// writes ONE matrix partial (on the group's first tile; the others flag zero
+// updates, so the relation-row pass skips them).  The blocks of the other tiles
+// exit at once.  Sums regroup (partials of up to tgroup tiles instead of one):
+// rounding-level differences only.
 template <typename T, bool PROJ, bool GRAD, int kNB>
 __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParBufs<T> bf) {
+    using M = Mfma16<T>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int t = a.tile_first[a.batch_seg[a.batch]] + blockIdx.x;
-    if (t >= a.tile_first[a.batch_seg[a.batch + 1]]) return;
-    int r, e0, cnt;
-    tile_range(a, t, r, e0, cnt);
+    const int t0 = a.tile_first[a.batch_seg[a.batch]] + blockIdx.x;
+    if (t0 >= a.tile_first[a.batch_seg[a.batch + 1]]) return;
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = lane_id();
+    const int G = nw == 8 && a.tgroup > 1 ? a.tgroup : 1;  // the register partial needs eight waves
+    const RTile tl0 = a.tiles[t0];
+    if (tl0.q % G != 0) return;  // another block runs this tile
+    const int ntl = min(G, a.tile_first[tl0.seg + 1] - t0);
     constexpr int NP = 16 * kNB, L = NP + 2;  // kNB = rm_np(n) / 16, exactly
     const int n = a.n, ld = a.ld;
     const int MV = rm_up16(4 * a.St), UY = rm_up16(2 * a.St);
@@ -194,145 +205,193 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
     T* coef = D + (GRAD ? UY * L : 0);
     int* ids = (int*)(coef + UY);  // entity of every V row
     int* kks = ids + MV;           // sample index of every tile sample
-    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = lane_id();
-    // samples of the tile: ids resolved by one thread each, then the rows gathered by all
-    for (int row = threadIdx.x; row < MV; row += blockDim.x) {
-        const int q = row >> 2, which = row & 3;
-        int e = -1;
-        if (q < cnt) {
-            const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
-            if (which == 0) kks[q] = kk;
-            const int i0 = a.si[kk], jj = a.sj[kk];
-            const int h = a.heads[i0], tt = a.tails[i0];
-            e = which == 0 ? h : which == 1 ? tt : which == 2 ? (a.side[kk] ? h : jj) : (a.side[kk] ? jj : tt);
+    // the group's matrix partial: wave w holds output tiles w, w + 8, ... of the kNB x kNB grid
+    constexpr int kAcc = (kNB * kNB + 7) / 8;
+    typename M::acc_t gacc[kAcc];
+#pragma unroll
+    for (int k = 0; k < kAcc; ++k) gacc[k] = typename M::acc_t{T(0), T(0), T(0), T(0)};
+    T dr[2] = {T(0), T(0)};  // wave 0: the relation-vector partial
+    int nact = 0;
+    for (int ti = 0; ti < ntl; ++ti) {
+        int r, e0, cnt;
+        tile_range(a, t0 + ti, r, e0, cnt);
+        // samples of the tile: ids resolved by one thread each, then the rows gathered by all
+        for (int row = threadIdx.x; row < MV; row += blockDim.x) {
+            const int q = row >> 2, which = row & 3;
+            int e = -1;
+            if (q < cnt) {
+                const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
+                if (which == 0) kks[q] = kk;
+                const int i0 = a.si[kk], jj = a.sj[kk];
+                const int h = a.heads[i0], tt = a.tails[i0];
+                e = which == 0 ? h : which == 1 ? tt : which == 2 ? (a.side[kk] ? h : jj) : (a.side[kk] ? jj : tt);
+            }
+            ids[row] = e;
         }
-        ids[row] = e;
-    }
-    if (PROJ) stage_matrix_padded<T, NP>(Wl, bf.W + (int64_t)r * n * ld, n, ld);
-    for (int idx = threadIdx.x; idx < UY * L; idx += blockDim.x) {
-        X[idx] = T(0);
-        if (GRAD) D[idx] = T(0);
-    }
-    for (int idx = threadIdx.x; idx < UY; idx += blockDim.x) coef[idx] = T(0);
-    __syncthreads();
-    if (PROJ) {  // V rows 4q + {0,1,2,3} = h, t, h', t' of sample q (zeros past the data)
-        gather_rows<T, NP>(V, ids, MV, bf.ent, n, ld);
-    }
-    __syncthreads();
-    if (PROJ) {
-        block_gemm_k<T, NP>(MV / 16, kNB, rm_k4(n), [&](int m, int k) { return V[m * L + k]; },
-                      [&](int k, int c) { return Wl[k * L + c]; }, [&](int m, int c, T v) { P[m * L + c] = v; });
+        if (PROJ && ti == 0) stage_matrix_padded<T, NP>(Wl, bf.W + (int64_t)r * n * ld, n, ld);
+        for (int idx = threadIdx.x; idx < UY * L; idx += blockDim.x) {
+            X[idx] = T(0);
+            if (GRAD) D[idx] = T(0);
+        }
+        for (int idx = threadIdx.x; idx < UY; idx += blockDim.x) coef[idx] = T(0);
         __syncthreads();
-        // one wave per sample: energies, hinge, x, d (transr/trainer.cpp:147-164, transr/transr.cpp:26-35)
-        for (int q = w; q < cnt; q += nw) {
-            const int kk = kks[q];
-            const T* ph = P + (4 * q + 0) * L;
-            const T* pt = P + (4 * q + 1) * L;
-            const T* pnh = P + (4 * q + 2) * L;
-            const T* pnt = P + (4 * q + 3) * L;
-            T vr[2];
-            lane_pair_load(bf.rel + (int64_t)r * ld, n, vr);
-            T ep = T(0), en = T(0), xp[2], xn[2];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int i = 2 * l + k;
-                const bool ok = i < n;
-                const T dp = ok ? pt[i] - ph[i] - vr[k] : T(0);
-                const T dn = ok ? pnt[i] - pnh[i] - vr[k] : T(0);
-                ep += a.l1 ? fabs(dp) : dp * dp;
-                en += a.l1 ? fabs(dn) : dn * dn;
-                xp[k] = ok ? (a.l1 ? (dp > T(0) ? T(1) : T(-1)) : T(2) * dp) : T(0);
-                xn[k] = ok ? (a.l1 ? (dn > T(0) ? T(1) : T(-1)) : T(2) * dn) : T(0);
-            }
-            T dpos[2], dneg[2];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int i = 2 * l + k;
-                dpos[k] = i < n ? V[(4 * q + 0) * L + i] - V[(4 * q + 1) * L + i] : T(0);
-                dneg[k] = i < n ? V[(4 * q + 2) * L + i] - V[(4 * q + 3) * L + i] : T(0);
-            }
-            lane_pair_store(bf.x + ((int64_t)kk * 2 + 0) * ld, n, xp);
-            lane_pair_store(bf.x + ((int64_t)kk * 2 + 1) * ld, n, xn);
-            lane_pair_store(bf.d + ((int64_t)kk * 2 + 0) * ld, n, dpos);
-            lane_pair_store(bf.d + ((int64_t)kk * 2 + 1) * ld, n, dneg);
-            lane_pair_store(X + (2 * q + 0) * L, n, xp);
-            lane_pair_store(X + (2 * q + 1) * L, n, xn);
-            if (a.compat) {
-                double* pr = a.proj + (int64_t)kk * 4 * ld;
+        if (PROJ) {  // V rows 4q + {0,1,2,3} = h, t, h', t' of sample q (zeros past the data)
+            gather_rows<T, NP>(V, ids, MV, bf.ent, n, ld);
+            __syncthreads();
+            block_gemm_k<T, NP>(MV / 16, kNB, rm_k4(n), [&](int m, int k) { return V[m * L + k]; },
+                          [&](int k, int c) { return Wl[k * L + c]; }, [&](int m, int c, T v) { P[m * L + c] = v; });
+            __syncthreads();
+            // one wave per sample: energies, hinge, x, d (transr/trainer.cpp:147-164, transr/transr.cpp:26-35)
+            for (int q = w; q < cnt; q += nw) {
+                const int kk = kks[q];
+                const T* ph = P + (4 * q + 0) * L;
+                const T* pt = P + (4 * q + 1) * L;
+                const T* pnh = P + (4 * q + 2) * L;
+                const T* pnt = P + (4 * q + 3) * L;
+                T vr[2];
+                lane_pair_load(bf.rel + (int64_t)r * ld, n, vr);
+                T ep = T(0), en = T(0), xp[2], xn[2];
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
                     const int i = 2 * l + k;
-                    if (i >= n) continue;
-                    pr[i] = (double)ph[i];
-                    pr[ld + i] = (double)pt[i];
-                    pr[2 * ld + i] = (double)pnh[i];
-                    pr[3 * ld + i] = (double)pnt[i];
+                    const bool ok = i < n;
+                    const T dp = ok ? pt[i] - ph[i] - vr[k] : T(0);
+                    const T dn = ok ? pnt[i] - pnh[i] - vr[k] : T(0);
+                    ep += a.l1 ? fabs(dp) : dp * dp;
+                    en += a.l1 ? fabs(dn) : dn * dn;
+                    xp[k] = ok ? (a.l1 ? (dp > T(0) ? T(1) : T(-1)) : T(2) * dp) : T(0);
+                    xn[k] = ok ? (a.l1 ? (dn > T(0) ? T(1) : T(-1)) : T(2) * dn) : T(0);
                 }
-            } else {
-                ep = wave_sum(ep);
-                en = wave_sum(en);
-                const bool active = (double)ep + a.margin > (double)en;
-                if (l == 0) {
-                    a.act[kk] = active ? 1 : 0;
-                    a.loss[kk] = active ? a.margin + (double)ep - (double)en : 0.0;
+                T dpos[2], dneg[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int i = 2 * l + k;
+                    dpos[k] = i < n ? V[(4 * q + 0) * L + i] - V[(4 * q + 1) * L + i] : T(0);
+                    dneg[k] = i < n ? V[(4 * q + 2) * L + i] - V[(4 * q + 3) * L + i] : T(0);
                 }
-                if (GRAD) {
+                lane_pair_store(bf.x + ((int64_t)kk * 2 + 0) * ld, n, xp);
+                lane_pair_store(bf.x + ((int64_t)kk * 2 + 1) * ld, n, xn);
+                lane_pair_store(bf.d + ((int64_t)kk * 2 + 0) * ld, n, dpos);
+                lane_pair_store(bf.d + ((int64_t)kk * 2 + 1) * ld, n, dneg);
+                lane_pair_store(X + (2 * q + 0) * L, n, xp);
+                lane_pair_store(X + (2 * q + 1) * L, n, xn);
+                if (a.compat) {
+                    double* pr = a.proj + (int64_t)kk * 4 * ld;
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const int i = 2 * l + k;
+                        if (i >= n) continue;
+                        pr[i] = (double)ph[i];
+                        pr[ld + i] = (double)pt[i];
+                        pr[2 * ld + i] = (double)pnh[i];
+                        pr[3 * ld + i] = (double)pnt[i];
+                    }
+                } else {
+                    ep = wave_sum(ep);
+                    en = wave_sum(en);
+                    const bool active = (double)ep + a.margin > (double)en;
+                    if (l == 0) {
+                        a.act[kk] = active ? 1 : 0;
+                        a.loss[kk] = active ? a.margin + (double)ep - (double)en : 0.0;
+                    }
+                    if (GRAD) {
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+                            const T c = active ? (T)(-(u ? 1.0 : -1.0) * a.lr) : T(0);  // -lr beta
+                            const T* dv = u ? dneg : dpos;
+                            const T dsc[2] = {c * dv[0], c * dv[1]};
+                            lane_pair_store(D + (2 * q + u) * L, n, dsc);
+                            if (l == 0) coef[2 * q + u] = c;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            // y = W x for every update (transr/trainer.cpp:168-169): Y = X W^T
+            block_gemm_k<T, NP>(UY / 16, kNB, rm_k4(n), [&](int m, int k) { return X[m * L + k]; },
+                          [&](int k, int c) { return Wl[c * L + k]; }, [&](int m, int c, T v) {
+                              if (m < 2 * cnt && c < n) bf.y[((int64_t)kks[m >> 1] * 2 + (m & 1)) * ld + c] = v;
+                          });
+        }
+        if (GRAD) {
+            if (!PROJ) {  // compat: directions from phase A, hinge from the work-vector scan
+                for (int q = w; q < cnt; q += nw) {
+                    const int kk = kks[q];
+                    const bool act = a.act[kk] != 0;
 #pragma unroll
                     for (int u = 0; u < 2; ++u) {
-                        const T c = active ? (T)(-(u ? 1.0 : -1.0) * a.lr) : T(0);  // -lr beta
-                        const T* dv = u ? dneg : dpos;
-                        const T dsc[2] = {c * dv[0], c * dv[1]};
-                        lane_pair_store(D + (2 * q + u) * L, n, dsc);
+                        const T c = act ? (T)(-(u ? 1.0 : -1.0) * a.lr) : T(0);
+                        T xv[2], dv[2];
+                        lane_pair_load(bf.x + ((int64_t)kk * 2 + u) * ld, n, xv);
+                        lane_pair_load(bf.d + ((int64_t)kk * 2 + u) * ld, n, dv);
+                        dv[0] *= c;
+                        dv[1] *= c;
+                        lane_pair_store(X + (2 * q + u) * L, n, xv);
+                        lane_pair_store(D + (2 * q + u) * L, n, dv);
                         if (l == 0) coef[2 * q + u] = c;
                     }
                 }
             }
+            __syncthreads();
+            // dW[j][i] = sum_u D[u][j] X[u][i]  (transr/trainer.cpp:166-167)
+            if (nw == 8) {  // into the group's register partial
+                const int K4 = (2 * cnt + 3) & ~3, kq = l >> 4, c16 = l & 15;
+#pragma unroll
+                for (int k = 0; k < kAcc; ++k) {
+                    const int idx = w + 8 * k;
+                    if (idx >= kNB * kNB) continue;
+                    const int jc = (idx / kNB) * 16 + c16, ic = (idx % kNB) * 16 + c16;
+                    for (int kb = 0; kb < K4; kb += 16) {
+                        T av[4], bv[4];
+#pragma unroll
+                        for (int s = 0; s < 4; ++s) {
+                            const int u = kb + 4 * s + kq;
+                            av[s] = u < UY ? D[u * L + jc] : T(0);
+                            bv[s] = u < UY ? X[u * L + ic] : T(0);
+                        }
+#pragma unroll
+                        for (int s = 0; s < 4; ++s)
+                            if (kb + 4 * s < K4) gacc[k] = M::mma(av[s], bv[s], gacc[k]);
+                    }
+                }
+            } else {  // four waves: one tile a block, written directly
+                T* wp = bf.wpart + (int64_t)blockIdx.x * n * ld;
+                block_gemm<T>(kNB, kNB, UY, [&](int j, int u) { return D[u * L + j]; },
+                              [&](int u, int i) { return X[u * L + i]; }, [&](int j, int i, T v) {
+                                  if (j < n && i < n) wp[(int64_t)j * ld + i] = v;
+                              });
+            }
+            if (w == 0) {  // dr = sum_u (-lr beta) x_u
+                for (int u = 0; u < 2 * cnt; ++u) {
+                    const T c = coef[u];
+                    dr[0] += c * X[u * L + 2 * l];
+                    dr[1] += c * X[u * L + 2 * l + 1];
+                    nact += c != T(0);
+                }
+            }
         }
-        __syncthreads();
-        // y = W x for every update (transr/trainer.cpp:168-169): Y = X W^T
-        block_gemm_k<T, NP>(UY / 16, kNB, rm_k4(n), [&](int m, int k) { return X[m * L + k]; },
-                      [&](int k, int c) { return Wl[c * L + k]; }, [&](int m, int c, T v) {
-                          if (m < 2 * cnt && c < n) bf.y[((int64_t)kks[m >> 1] * 2 + (m & 1)) * ld + c] = v;
-                      });
+        if (ti + 1 < ntl) __syncthreads();  // the next tile's ids, X, D
     }
     if (!GRAD) return;
-    if (!PROJ) {  // compat: directions from phase A, hinge from the work-vector scan
-        for (int q = w; q < cnt; q += nw) {
-            const int kk = kks[q];
-            const bool act = a.act[kk] != 0;
+    if (nw == 8) {
+        T* wp = bf.wpart + (int64_t)blockIdx.x * n * ld;
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const T c = act ? (T)(-(u ? 1.0 : -1.0) * a.lr) : T(0);
-                T xv[2], dv[2];
-                lane_pair_load(bf.x + ((int64_t)kk * 2 + u) * ld, n, xv);
-                lane_pair_load(bf.d + ((int64_t)kk * 2 + u) * ld, n, dv);
-                dv[0] *= c;
-                dv[1] *= c;
-                lane_pair_store(X + (2 * q + u) * L, n, xv);
-                lane_pair_store(D + (2 * q + u) * L, n, dv);
-                if (l == 0) coef[2 * q + u] = c;
+        for (int k = 0; k < kAcc; ++k) {
+            const int idx = w + 8 * k;
+            if (idx >= kNB * kNB) continue;
+            const int i = (idx % kNB) * 16 + (l & 15);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j = (idx / kNB) * 16 + M::row(l, q);
+                if (j < n && i < n) wp[(int64_t)j * ld + i] = gacc[k][q];
             }
         }
     }
-    __syncthreads();
-    // dW[j][i] = sum_u D[u][j] X[u][i]  (transr/trainer.cpp:166-167), this tile's partial
-    T* wp = bf.wpart + (int64_t)blockIdx.x * n * ld;
-    block_gemm<T>(kNB, kNB, UY, [&](int j, int u) { return D[u * L + j]; },
-                  [&](int u, int i) { return X[u * L + i]; }, [&](int j, int i, T v) {
-                      if (j < n && i < n) wp[(int64_t)j * ld + i] = v;
-                  });
-    if (w == 0) {  // dr = sum_u (-lr beta) x_u
-        T acc[2] = {T(0), T(0)};
-        for (int u = 0; u < 2 * cnt; ++u) {
-            const T c = coef[u];
-            acc[0] += c * X[u * L + 2 * l];
-            acc[1] += c * X[u * L + 2 * l + 1];
-        }
-        lane_pair_store(bf.rpart + (int64_t)blockIdx.x * ld, n, acc);
+    if (w == 0) {
+        lane_pair_store(bf.rpart + (int64_t)blockIdx.x * ld, n, dr);
         if (l == 0) {
-            int nact = 0;
-            for (int u = 0; u < 2 * cnt; ++u) nact += coef[u] != T(0);
-            a.tile_act[t] = nact;
+            a.tile_act[t0] = nact;
+            for (int ti = 1; ti < ntl; ++ti) a.tile_act[t0 + ti] = 0;  // the group's partial is on t0
         }
     }
 }

@@ -47,6 +47,7 @@ struct RParArgs {
     const uint8_t* side;
     int32_t B, n, ld, ne, nr, St;
     int32_t batch;
+    int32_t tgroup;  // matrix-core tile kernels: tiles a workgroup runs (one partial per group; 0, 1: one)
     double lr, margin;
     int32_t compat, l1;
     // event index
@@ -461,9 +462,10 @@ __device__ __forceinline__ void transr_rel_rows_wave(RParArgs a, RParBufs<T> bf,
     T v[2];
     lane_pair_load(row, n, v);
     for (int base = u0; base < u1; base += kWave) {
-        // every tile's partial (the VALU transRNorm step writes one for each
-        // tile), or only the flagged ones of the matrix-core transRNorm step
-        uint64_t m = sel ? flags(base) : (uint64_t)__ballot(base + lane_id() < u1);
+        // every tile's partial for the VALU transRNorm step (it writes one for each
+        // tile); the flagged ones otherwise: the gradient step's inactive tiles carry
+        // zeros and a matrix-core tile group's partial sits on its first tile alone
+        uint64_t m = (NORM || sel) ? flags(base) : (uint64_t)__ballot(base + lane_id() < u1);
         while (m) {  // eight partial rows in flight, summed in slot order
             T p[8][2];
             bool use[8];
