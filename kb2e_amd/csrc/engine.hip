@@ -1685,7 +1685,11 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
                 fprintf(stderr, "rpar_cons chunk kernel: relations %llu, chunks %llu (most in a relation %llu), "
                         "violators %llu, rounds %llu (most %llu), cycles mean %.0f max %llu\n", q[0], q[1], q[6], q[2],
                         q[3], q[7], q[0] ? (double)q[4] / (double)q[0] : 0.0, q[5]);
-                if (c->rpar_cons_wide)
+                if (c->rpar_cons_wide && cons_chainw_pipelined(c->n))
+                    fprintf(stderr, "rpar_cons pipelined wide chain phases (walker: prologue+K0, window list, walk, "
+                            "B1 wait, row stores+fold, B2 wait, drain, window flags, tail, write-back, -; helper: "
+                            "debt+fold+B2, X tile, B1 wait, -, -, -):");
+                else if (c->rpar_cons_wide)
                     fprintf(stderr, "rpar_cons wide chain phases (prologue, window list, rows+barrier, P+Gram+B1, "
                             "K0, V+sums, B(1), rounds+g, B(2), later pairs, B(3), records+W update, chunk barrier, "
                             "window flags, tail, write-back):");

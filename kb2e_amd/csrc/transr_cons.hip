@@ -13,6 +13,7 @@
 #include "kernels_transr_cons.hpp"
 #include "kernels_transr_seq.hpp"
 #include "kernels_transr_chainw.hpp"
+#include "kernels_transr_chainwp.hpp"
 #include "kernels_transr_pipe.hpp"
 #include "kernels_transr_wave.hpp"
 
@@ -81,6 +82,24 @@ const void* chainw_fn(int n) {
     throw std::runtime_error("transRNorm wide chain kernel: n > 112");
 }
 
+const void* chainwp_fn(int n) {
+    switch (wp_ks(n)) {
+        case 18: return (const void*)transr_cons_chain_wpipe_kernel<18>;
+        case 20: return (const void*)transr_cons_chain_wpipe_kernel<20>;
+        case 22: return (const void*)transr_cons_chain_wpipe_kernel<22>;
+        case 24: return (const void*)transr_cons_chain_wpipe_kernel<24>;
+        case 25: return (const void*)transr_cons_chain_wpipe_kernel<25>;
+    }
+    throw std::runtime_error("transRNorm pipelined wide chain kernel: no instantiation");
+}
+
+// 64 < n <= 100: the pipelined wide chain (kernels_transr_chainwp.hpp);
+// KB2E_RPAR_CHAIN=lockstep keeps the eight-wave lockstep kernel (A/B)
+bool use_wpipe(int n) {
+    const char* e = getenv("KB2E_RPAR_CHAIN");
+    return n > 64 && n <= kWPMaxN && !(e && (std::string(e) == "lockstep" || std::string(e) == "wide"));
+}
+
 // KB2E_RPAR_CHAIN=serial: the unpipelined chain kernel (kernels_transr_seq.hpp)
 bool use_pipe() {
     const char* e = getenv("KB2E_RPAR_CHAIN");
@@ -112,10 +131,14 @@ void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, int grid, si
 bool cons_chainw_supported(int n) { return n >= 1 && n <= kWideMaxN; }
 
 size_t cons_chainw_setup(int n) {
-    const size_t lds = chainw_lds(n);
-    HIPCHK(hipFuncSetAttribute(chainw_fn(n), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const bool wp = use_wpipe(n);
+    const size_t lds = wp ? chainwp_lds(n) : chainw_lds(n);
+    HIPCHK(hipFuncSetAttribute(wp ? chainwp_fn(n) : chainw_fn(n), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
     return lds;
 }
+
+bool cons_chainw_pipelined(int n) { return use_wpipe(n); }
 
 void cons_chainw_launch(const RParArgs& a, const RParBufs<double>& bf, size_t lds, hipStream_t stream) {
     RParArgs aa = a;
@@ -123,7 +146,9 @@ void cons_chainw_launch(const RParArgs& a, const RParBufs<double>& bf, size_t ld
     void* args[] = {&aa, &bb};
     // one workgroup per relation, most frequent first (those absent from the batch exit)
     const int grid = a.nr;
-    HIPCHK(hipLaunchKernel(chainw_fn(a.n), dim3(grid), dim3(kWideThreads), args, lds, stream));
+    // (the LDS size was chosen by cons_chainw_setup under the same switch)
+    if (use_wpipe(a.n)) HIPCHK(hipLaunchKernel(chainwp_fn(a.n), dim3(grid), dim3(kWPThreads), args, lds, stream));
+    else HIPCHK(hipLaunchKernel(chainw_fn(a.n), dim3(grid), dim3(kWideThreads), args, lds, stream));
     const int da_grid = (int)(((int64_t)4 * a.B + a.nr + 3) / 4);  // a wave a record
     HIPCHK(hipLaunchKernel((const void*)transr_cons_da_wide_kernel, dim3(da_grid), dim3(256), args, 0, stream));
 }

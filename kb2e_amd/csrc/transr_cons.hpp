@@ -33,13 +33,17 @@ void grad_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, hipStr
 // the pair records' kernel after it.
 size_t cons_seq_setup(int n);
 void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, int grid, size_t lds, hipStream_t stream);
-// transRNorm per relation, pair by pair, for n <= 112 (kernels_transr_chainw.hpp; FP64,
+// transRNorm per relation, pair by pair, for n <= 112 (kernels_transr_chainw.hpp,
+// kernels_transr_chainwp.hpp; FP64,
 // any path: the VALU tile kernels at n = 100): is the width covered, its dynamic LDS
 // (the limit raised to it), and the launch of the chain (one workgroup per relation
 // segment of the batch) and of its pair records' kernel.
 bool cons_chainw_supported(int n);
 size_t cons_chainw_setup(int n);
 void cons_chainw_launch(const RParArgs& a, const RParBufs<double>& bf, size_t lds, hipStream_t stream);
+// Does that chain run software-pipelined at this width (64 < n <= 100,
+// kernels_transr_chainwp.hpp; KB2E_RPAR_CHAIN=lockstep: the eight-wave lockstep kernel)?
+bool cons_chainw_pipelined(int n);
 // The chunk kernel's counters (relations, chunks, violators, rounds, cycles sum / max,
 // most chunks of a relation), reset.
 void cons_seq_take_stats(unsigned long long (&st)[64]);

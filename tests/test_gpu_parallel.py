@@ -86,7 +86,8 @@ def _cons_form(dim, mfma):
     """The transRNorm form the engine runs (engine_transr_parallel.inc): the
     per-relation sequential chain (every pair against the matrix the earlier
     ones left) in FP64 up to n = 112 -- kernels_transr_seq.hpp / _pipe.hpp on
-    the n <= 64 matrix-core path, kernels_transr_chainw.hpp elsewhere -- unless
+    the n <= 64 matrix-core path, kernels_transr_chainwp.hpp at 64 < n <= 100,
+    kernels_transr_chainw.hpp elsewhere -- unless
     KB2E_RPAR_CONS picks the Jacobi tile / wave kernels; Jacobi above 112."""
     ck = os.environ.get("KB2E_RPAR_CONS", "")
     if ck in ("tile", "jacobi") or dim > 112:
@@ -177,14 +178,19 @@ def test_transr_parallel_chain_windows(dim, compat, env, St, chain, monkeypatch)
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=compat)
 
 
+@pytest.mark.parametrize("chain", ["default", "lockstep"])
 @pytest.mark.parametrize("dim,compat,mfma", [(100, True, False), (100, False, False), (72, True, True),
-                                             (20, True, False)])
-def test_transr_parallel_wide_chain_windows(dim, compat, mfma, monkeypatch):
-    """The wide chain kernel (kernels_transr_chainw.hpp) over several 256-sample
-    windows of a relation: the small set's hottest relation holds ~700 samples
-    a batch (B = 3,000), so W_c, K0 and the held-back tail (the relation's last
-    update) carry across windows; n = 20 on the VALU path runs it at one column
-    tile."""
+                                             (20, True, False), (88, False, True)])
+def test_transr_parallel_wide_chain_windows(dim, compat, mfma, chain, monkeypatch):
+    """The wide chain kernels over several windows of a relation (256 samples
+    for the pipelined kernel, kernels_transr_chainwp.hpp, the default at
+    64 < n <= 100; 512 for the lockstep one, kernels_transr_chainw.hpp,
+    KB2E_RPAR_CHAIN=lockstep): the small set's hottest relation holds ~700
+    samples a batch (B = 3,000), so W_c, K0, the pipeline's pending W update and
+    the held-back tail (the relation's last update) carry across windows; n = 20
+    on the VALU path runs the lockstep kernel at one column tile either way."""
+    if chain == "lockstep":
+        monkeypatch.setenv("KB2E_RPAR_CHAIN", "lockstep")
     _transr_vs_model(data.synthetic("small", seed=1), dim, 1, monkeypatch, St=2 if mfma else 8, compat=compat,
                      mfma=mfma, rate=0.001)
 

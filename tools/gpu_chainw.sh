@@ -18,3 +18,7 @@ timeout -k 10 300 python -u bench.py --only --no-cpu-baseline --no-epoch --steps
 python3 -c "import json;d=json.load(open('$OUT/k4_bench.json'));print('K4',d['value'],d['ms_per_step'],d['roofline']['kernels_avg_us'])"
 KB2E_RPAR_CHAIN=wide timeout -k 10 300 python -u bench.py --only --no-cpu-baseline --no-epoch --steps 100 --warmup 100 > $OUT/k4_wide.json 2> $OUT/k4_wide.err || { echo "k4 wide bench failed $?"; tail -5 $OUT/k4_wide.err; exit 1; }
 python3 -c "import json;d=json.load(open('$OUT/k4_wide.json'));print('K4 wide',d['value'],d['ms_per_step'],d['roofline']['kernels_avg_us'])"
+KB2E_RPAR_TGROUP=1 timeout -k 10 400 python -u bench.py --config transr_k5 --only --no-cpu-baseline --no-epoch --steps 20 --warmup 5 > $OUT/k5_tg1.json 2> $OUT/k5_tg1.err || { echo "k5 tgroup=1 bench failed $?"; tail -5 $OUT/k5_tg1.err; exit 1; }
+python3 -c "import json;d=json.load(open('$OUT/k5_tg1.json'));print('K5 tgroup=1',d['value'],d['ms_per_step'],d['roofline']['kernels_avg_us'])"
+KB2E_RPAR_CHAIN=lockstep timeout -k 10 400 python -u bench.py --config transr_k5 --only --no-cpu-baseline --no-epoch --steps 20 --warmup 5 > $OUT/k5_lockstep.json 2> $OUT/k5_lockstep.err || { echo "k5 lockstep bench failed $?"; tail -5 $OUT/k5_lockstep.err; exit 1; }
+python3 -c "import json;d=json.load(open('$OUT/k5_lockstep.json'));print('K5 lockstep',d['value'],d['ms_per_step'],d['roofline']['kernels_avg_us'])"
