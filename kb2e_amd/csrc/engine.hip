@@ -170,7 +170,7 @@ struct kb2e_ctx {
     bool rpar_cons_wide = false;  // the same chain for n <= 112 off the n <= 64 matrix-core path (kernels_transr_chainw.hpp)
     size_t rpar_wide_lds = 0;
     DevBuf rpar_pflag, rpar_cons_tile, rpar_cpairs, rpar_cnrows;
-    DevBuf rpar_y, rpar_wpart, rpar_rpart, rpar_tile_act, rpar_pair, rpar_relpair, rpar_relpair_stamp, rpar_tiles,
+    DevBuf rpar_y, rpar_wpart, rpar_rpart, rpar_tile_act, rpar_pair, rpar_relpair, rpar_relpair_stamp, rpar_scan_pre, rpar_tiles,
         rpar_ntiles, rpar_tile_first, rpar_rel_begin, rpar_scan;
     DevBuf rpar_ptab;  // transRNorm pair dedupe: two per-batch (relation, entity) tables
     DevBuf rpar_batch_t0, rpar_td_r, rpar_td_cnt, rpar_td_kk, rpar_td_ent;  // per-epoch tile descriptors
@@ -1688,7 +1688,7 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
                 if (c->rpar_cons_wide && cons_chainw_pipelined(c->n))
                     fprintf(stderr, "rpar_cons pipelined wide chain phases (walker: prologue+K0, window list, walk, "
                             "B1 wait, row stores+fold, B2 wait, drain, window flags, tail, write-back, -; helper: "
-                            "debt+fold+B2, X tile, B1 wait, -, -, -):");
+                            "debt+fold+B2, X tile, B1 wait; walker: row+V, sums+rounds+g, later rows):");
                 else if (c->rpar_cons_wide)
                     fprintf(stderr, "rpar_cons wide chain phases (prologue, window list, rows+barrier, P+Gram+B1, "
                             "K0, V+sums, B(1), rounds+g, B(2), later pairs, B(3), records+W update, chunk barrier, "

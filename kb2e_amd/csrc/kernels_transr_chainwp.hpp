@@ -38,16 +38,17 @@ constexpr int kWPThreads = 512;       // eight waves: the walker and seven helpe
 constexpr int kWPRows = 16;           // pairs a chunk: one MFMA row tile
 constexpr int kWPWin = 256;           // samples a window
 constexpr int kWPPairs = 4 * kWPWin;  // pairs a window, at most
-constexpr int kWPMaxN = 100;          // K0 [100][101] + the buffers: 156 KiB
+constexpr int kWPMaxN = 100;          // K0 [100][100] + the buffers: 159 KiB
 
 __host__ __device__ constexpr int wp_ks(int n) {  // the k-steps: an instantiated KS >= ceil(n / 4)
     return n <= 72 ? 18 : n <= 80 ? 20 : n <= 88 ? 22 : n <= 96 ? 24 : 25;
 }
 
 // LDS bytes: K0 / W' [4 KS][4 KS + 2] | A [3][R][4 KS + 2] | P [2][R][4 KS + 2] |
-// qpart [R] ; ints pe, ps [kWPPairs] | vlist [2][R] | wsum [8] | misc [8] ; vflag [kWPPairs]
+// Gram [2][R][R + 1] | cross Gram [R][R + 1] | qpart [R] ; ints pe, ps [kWPPairs] | vlist [2][R] | wsum [8] | misc [8] ; vflag [kWPPairs]
 __host__ __device__ constexpr size_t chainwp_lds_ks(int KS) {
-    return sizeof(double) * ((size_t)(4 * KS) * (4 * KS + 2) + 5 * (size_t)kWPRows * (4 * KS + 2) + kWPRows) +
+    return sizeof(double) * ((size_t)(4 * KS) * (4 * KS + 2) + 5 * (size_t)kWPRows * (4 * KS + 2) +
+                             3 * (size_t)kWPRows * (kWPRows + 1) + kWPRows) +
            sizeof(int) * (2 * (size_t)kWPPairs + 2 * kWPRows + 16) + (size_t)kWPPairs;
 }
 __host__ __device__ constexpr size_t chainwp_lds(int n) { return chainwp_lds_ks(wp_ks(n)); }
@@ -58,7 +59,7 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
     using M = Mfma16<T>;
     constexpr int NC = 4 * KS;                 // the columns the chain keeps (>= n; zeros past n)
     constexpr int NB = (NC + 15) / 16;         // MFMA column tiles
-    constexpr int LA = NC + 2, LK = NC + 1, R = kWPRows, NT = kWPThreads, NW = NT / 64;
+    constexpr int LA = NC + 2, R = kWPRows, LG = R + 1, NT = kWPThreads, NW = NT / 64;
     static_assert(NB <= NW - 1, "a column tile a helper wave");
     static_assert(2 * R * LA >= NB * NC, "the renorm's row partials borrow the P buffers");
     // block b takes the b-th most frequent relation (the hot chains start first)
@@ -84,10 +85,12 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
     const int col = 16 * cb + l16;         // (helpers) the fragment column
     const T lr = (T)a.lr;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    T* K0 = (T*)smem;              // [NC][LA] W' (prologue), then K0 [NC][LK]
+    T* K0 = (T*)smem;              // [NC][LA] W' (prologue), then K0 as [NC / 2][NC] pairs (K0[2 i2 + e][c] at (i2 NC + c) 2 + e)
     T* Abuf = K0 + NC * LA;        // [3][R][LA] entity rows of chunks k - 1 / k + 2, k, k + 1
     T* Pbuf = Abuf + 3 * R * LA;   // [2][R][LA] projections of chunks k, k + 1 (violator rows: G)
-    T* qpart = Pbuf + 2 * R * LA;  // [R] |p_j|^2 of the next chunk
+    T* Gbuf = Pbuf + 2 * R * LA;   // [2][R][LG] Gram matrices A A^T of chunks k, k + 1
+    T* Cx = Gbuf + 2 * R * LG;     // [R][LG] cross Gram A_{k+1} A_k^T (next x current)
+    T* qpart = Cx + R * LG;        // [R] |p_j|^2 of the next chunk
     int* pe = (int*)(qpart + R);   // [kWPPairs]
     int* ps = pe + kWPPairs;       // [kWPPairs]
     int* vlist = ps + kWPPairs;    // [2][R] the violators of a chunk, by chunk parity
@@ -100,12 +103,13 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
     // >= 200 chunks also 24..39): 0 prologue + K0, 1 window list, 2 walk, 3 B1 wait,
     // 4 row stores + fold, 5 B2 wait, 6 drain, 7 window flags, 8 tail, 9 write-back;
     // thread 64 (helper wave 1): 10 debt (W update + records; from its last tick: the
-    // fold and B2 too), 11 X tile, 12 B1 wait
+    // fold and B2 too), 11 X tile, 12 B1 wait; the walk's violators split into 13
+    // (row to LDS + V), 14 (sums, rounds, g), 15 (later rows; phase 2 keeps the rest)
     __shared__ unsigned long long ph[16];
     if (tid < 16) ph[tid] = 0;
     long long tq = ck0;
     auto tick = [&](int k) {
-        if (bf.stats && (k < 10 ? tid == 0 : tid == 64)) {
+        if (bf.stats && ((k >= 10 && k <= 12) ? tid == 64 : tid == 0)) {
             const long long t = clock64();
             atomicAdd(&ph[k], (unsigned long long)(t - tq));
             tq = t;
@@ -178,9 +182,9 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int ri = 16 * ib + M::row(l, q);
-                if (ri < NC && cj < NC) {
-                    K0[ri * LK + cj] = kacc[t][q];
-                    K0[cj * LK + ri] = kacc[t][q];
+                if (ri < NC && cj < NC) {  // K0[i][c] at pair (i / 2, c), element i & 1
+                    K0[((ri >> 1) * NC + cj) * 2 + (ri & 1)] = kacc[t][q];
+                    K0[((cj >> 1) * NC + ri) * 2 + (cj & 1)] = kacc[t][q];
                 }
             }
         }
@@ -219,8 +223,10 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
             if (idx < R * NC) Abuf[slot * R * LA + (idx / NC) * LA + idx % NC] = ((rows_ok >> q) & 1) ? rows[q] : T(0);
         }
     };
-    // helpers: X = A W_c on their column tile (KS k-steps, B from the registers)
-    auto x_tile = [&](const T* Ar, T* out) {
+    // helpers: X = A W_c on their column tile (KS k-steps, B from the registers);
+    // wave 4 also the chunk's Gram matrix A A^T (its B operand is its A operand),
+    // wave 5 the cross Gram A A_c^T with the current chunk (Ac; none for a fresh chunk)
+    auto x_tile = [&](const T* Ar, T* out, T* G, const T* Ac) {
         if (!own) return;
         typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
         T av[KS];
@@ -231,6 +237,20 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
         if (col < NC) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) out[(kq + 4 * q) * LA + col] = acc[q];
+        }
+        if (w == 4) {
+            typename M::acc_t ga = {T(0), T(0), T(0), T(0)};
+#pragma unroll
+            for (int q = 0; q < KS; ++q) ga = M::mma(av[q], av[q], ga);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) G[(kq + 4 * q) * LG + l16] = ga[q];
+        }
+        if (w == 5 && Ac) {  // the cross Gram with the current chunk's rows (the fold's dots)
+            typename M::acc_t ca = {T(0), T(0), T(0), T(0)};
+#pragma unroll
+            for (int q = 0; q < KS; ++q) ca = M::mma(av[q], Ac[l16 * LA + 4 * q + kq], ca);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Cx[(kq + 4 * q) * LG + l16] = ca[q];
         }
     };
     // the helpers' debt: the pending chunk's W_c -= lr A^T G on their tile (G rows in
@@ -255,9 +275,9 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
         }
     };
     // all threads: P_n[j] -= lr sum_v (a_n[j] . a_v) g_v over the current chunk's nv
-    // violators (vl; a_v in Ac, g_v in Pc), then |p_j|^2 into qpart; 32 threads a
-    // row, four columns each
-    auto fold = [&](T* Pn, const T* An, int cn, int nv, const T* Pc, const T* Ac, const int* vl) {
+    // violators (vl; the dots from the cross Gram Cx, g_v in Pc), then |p_j|^2 into
+    // qpart; 32 threads a row, four columns each
+    auto fold = [&](T* Pn, int cn, int nv, const T* Pc, const int* vl) {
         const int j = tid >> 5, c0 = 4 * (tid & 31);
         const bool okr = j < cn && c0 < NC;
         T x[4] = {T(0), T(0), T(0), T(0)};
@@ -266,22 +286,10 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
             for (int u = 0; u < 4; ++u) x[u] = Pn[j * LA + c0 + u];
         }
         if (nv > 0) {
-            T an[4] = {T(0), T(0), T(0), T(0)};
-            if (okr) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) an[u] = An[j * LA + c0 + u];
-            }
             for (int k = 0; k < nv; ++k) {
                 const int v = vl[k];
-                T d = T(0);
                 if (okr) {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) d = fma(an[u], Ac[v * LA + c0 + u], d);
-                }
-#pragma unroll
-                for (int m = 1; m < 32; m <<= 1) d += __shfl_xor(d, m);
-                if (okr) {
-                    const T gl = -lr * d;
+                    const T gl = -lr * Cx[j * LG + v];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) x[u] = fma(gl, Pc[v * LA + c0 + u], x[u]);
                 }
@@ -322,7 +330,7 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
     };
     // the walk of one chunk (wave 0): pairs [base, base + cc), projections in P (rows
     // j < cc), |p_j|^2 in qpart, rows in A; the violators' rows of P become G
-    auto walk = [&](T* P, const T* A, int cc, int base, int* vl) {
+    auto walk = [&](T* P, const T* Gm, int cc, int base, int* vl) {
         const int j = l & (R - 1), h = l >> 4;  // lane: quarter h of row j
         T q = j < cc ? qpart[j] : T(0);
         uint32_t vmask = 0;
@@ -342,33 +350,50 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
 #pragma unroll
                     for (int u = 0; u < KS; ++u) P[v * LA + h * KS + u] = x[u];
                 }
-                // a_j . a_v for every row (quarters, then the four lanes of a row)
-                T dp = T(0);
-#pragma unroll 5
-                for (int u = 0; u < KS; ++u) dp = fma(A[j * LA + h * KS + u], A[v * LA + h * KS + u], dp);
-                dp += __shfl_xor(dp, 16);
-                dp += __shfl_xor(dp, 32);
-                // V_c = sum_i p_v[i] K0[i][c], c = l and l + 64
+                // a_j . a_v for every row, from the chunk's Gram matrix
+                const T dp = Gm[j * LG + v];
+                // V_c = sum_i p_v[i] K0[i][c], c = l and l + 64: 16-byte reads of K0's row
+                // pairs (consecutive lanes, consecutive pairs), p_v as broadcasts; the
+                // second column's reads are clamped, not branched (its lanes >= NC - 64
+                // discard the sums)
                 const T* pr = P + v * LA;
+                const double2* kp = (const double2*)K0;
+                const double2* pp2 = (const double2*)pr;
+                const int c1r = c1 < NC ? c1 : l;
                 T va[4] = {T(0), T(0), T(0), T(0)}, vb[4] = {T(0), T(0), T(0), T(0)};
+                // software-pipelined: the next four rows' six 16-byte reads are in flight
+                // while the current four rows' FMAs run (one LDS round trip per two steps)
+                double2 cur[6], nxt[6];
+                auto ld6 = [&](int i2, double2 (&d)[6]) {
+                    d[0] = pp2[i2];
+                    d[1] = pp2[i2 + 1];
+                    d[2] = kp[i2 * NC + l];
+                    d[3] = kp[(i2 + 1) * NC + l];
+                    d[4] = kp[i2 * NC + c1r];
+                    d[5] = kp[(i2 + 1) * NC + c1r];
+                };
+                auto fm6 = [&](const double2 (&d)[6]) {
+                    va[0] = fma(d[0].x, d[2].x, va[0]);
+                    va[1] = fma(d[0].y, d[2].y, va[1]);
+                    va[2] = fma(d[1].x, d[3].x, va[2]);
+                    va[3] = fma(d[1].y, d[3].y, va[3]);
+                    vb[0] = fma(d[0].x, d[4].x, vb[0]);
+                    vb[1] = fma(d[0].y, d[4].y, vb[1]);
+                    vb[2] = fma(d[1].x, d[5].x, vb[2]);
+                    vb[3] = fma(d[1].y, d[5].y, vb[3]);
+                };
+                ld6(0, cur);
 #pragma unroll 2
-                for (int i = 0; i < NC; i += 4) {  // (NC = 4 KS: whole steps of four rows)
-                    const double2 pa = *(const double2*)(pr + i);
-                    const double2 pb = *(const double2*)(pr + i + 2);
-                    const T* kr = K0 + i * LK;
-                    va[0] = fma(pa.x, kr[l], va[0]);
-                    va[1] = fma(pa.y, kr[LK + l], va[1]);
-                    va[2] = fma(pb.x, kr[2 * LK + l], va[2]);
-                    va[3] = fma(pb.y, kr[3 * LK + l], va[3]);
-                    if (c1 < NC) {
-                        vb[0] = fma(pa.x, kr[c1], vb[0]);
-                        vb[1] = fma(pa.y, kr[LK + c1], vb[1]);
-                        vb[2] = fma(pb.x, kr[2 * LK + c1], vb[2]);
-                        vb[3] = fma(pb.y, kr[3 * LK + c1], vb[3]);
-                    }
+                for (int i2 = 2; i2 < NC / 2; i2 += 2) {  // (NC = 4 KS: whole steps of four rows)
+                    ld6(i2, nxt);
+                    fm6(cur);
+#pragma unroll
+                    for (int t = 0; t < 6; ++t) cur[t] = nxt[t];
                 }
+                fm6(cur);
                 const T V0 = (va[0] + va[1]) + (va[2] + va[3]);
-                const T V1 = (vb[0] + vb[1]) + (vb[2] + vb[3]);
+                const T V1 = c1 < NC ? (vb[0] + vb[1]) + (vb[2] + vb[3]) : T(0);
+                tick(13);
                 const T pv0 = pr[l], pv1 = c1 < NC ? pr[c1] : T(0);
                 T s2[2] = {pv0 * V0 + pv1 * V1, V0 * V0 + V1 * V1};
                 wave_sums<T, 2>(s2);
@@ -388,6 +413,7 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
                 // g (zero past n: p and K0 are); the violator's row now holds G
                 P[v * LA + l] = cpf * pv0 - cvf * (V0 + aa * pv0);
                 if (c1 < NC) P[v * LA + c1] = cpf * pv1 - cvf * (V1 + aa * pv1);
+                tick(14);
                 // the later rows: p_j -= lr (a_j . a_v) g, |p_j|^2 afresh
                 const bool upd = j > v && j < cc;
                 T qh = T(0);
@@ -407,6 +433,7 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
                 vmask |= 1u << v;
                 cursor = v + 1;
                 ++n_vio;
+                tick(15);
             }
         }
         if (l < R && ((vmask >> l) & 1u)) {
@@ -431,9 +458,9 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
         }
         if (nch > 2) load_rows(2 * R, 2 * R + csz(2));
         __syncthreads();
-        x_tile(Abuf, Pbuf);  // chunk 0 afresh
+        x_tile(Abuf, Pbuf, Gbuf, nullptr);  // chunk 0 afresh
         __syncthreads();
-        fold(Pbuf, Abuf, csz(0), 0, nullptr, nullptr, nullptr);
+        fold(Pbuf, csz(0), 0, nullptr, nullptr);
         __syncthreads();
         for (int k = 0; k < nch; ++k) {
             const int cc = csz(k), cn = csz(k + 1);
@@ -442,19 +469,25 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
             const T* An = Abuf + kn * R * LA;
             T* P = Pbuf + pc * R * LA;
             T* Pn = Pbuf + (pc ^ 1) * R * LA;
+            const T* Gm = Gbuf + pc * R * LG;
+            T* Gn = Gbuf + (pc ^ 1) * R * LG;
             int* vl = vlist + pc * R;
             ++n_chunks;
             if (w == 0) {
-                walk(P, A, cc, k * R, vl);
+                walk(P, Gm, cc, k * R, vl);
                 tick(2);
             } else {
                 apply_pending();  // chunk k - 1's
                 tick(10);
-                if (cn > 0) x_tile(An, Pn);
+                if (cn > 0 && !(bf.dbg & 1)) x_tile(An, Pn, Gn, A);
                 tick(11);
             }
             __syncthreads();  // B1: the walk's G rows and violators, X_{k+1}
             tick(w == 0 ? 3 : 12);
+            if (bf.dbg & 1) {  // (timing experiment: the projections after the walk, not beside it)
+                if (w > 0 && cn > 0) x_tile(An, Pn, Gn, A);
+                __syncthreads();
+            }
             const int nv = misc[2];
             pend_nv = nv;
             pend_par = pc;
@@ -467,7 +500,7 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
                 store_rows((k + 2) % 3);
                 if (k + 3 < nch) load_rows((k + 3) * R, (k + 3) * R + csz(k + 3));
             }
-            if (cn > 0) fold(Pn, An, cn, nv, P, A, vl);
+            if (cn > 0) fold(Pn, cn, nv, P, vl);
             tick(4);
             __syncthreads();  // B2: P_{k+1} and its |p|^2
             tick(5);

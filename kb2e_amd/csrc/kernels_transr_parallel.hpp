@@ -973,8 +973,52 @@ static __attribute__((unused)) __global__ __launch_bounds__(256) void rpar_scan_
     }
 }
 
+// Many chunks (K5: 5,000 a batch): the exclusive prefix over the chunks once for
+// all, pre[c][e] = work_in[e] + sum_{c' < c} sums[c'][e], instead of every block
+// summing all earlier chunks (quadratic in the chunks: ~20 GB of L2 reads a K5
+// batch).  A block takes 32 elements, 32 threads an element each over a
+// contiguous run of chunks: run totals, their exclusive scan, then the prefix
+// written along each run (rows of 32 consecutive elements: 256-byte accesses).
+constexpr int kScanDirectMax = 256;  // chunks up to which every block sums its own prefix
+
+static __attribute__((unused)) __global__ __launch_bounds__(1024) void rpar_scan_prefix_kernel(
+    const double* sums, int32_t nchunks, int32_t E2, const double* work_in, double* pre) {
+    __shared__ double tot[32][33];
+    const int el = threadIdx.x & 31, part = threadIdx.x >> 5;
+    const int e = blockIdx.x * 32 + el;
+    const int per = (nchunks + 31) / 32;
+    const int c0 = part * per, c1 = min(nchunks, c0 + per);
+    double s = 0.0;
+    if (e < E2) {
+        for (int c = c0; c < c1; c += 8) {
+            double v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = c + q < c1 ? sums[(int64_t)(c + q) * E2 + e] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) s += v[q];
+        }
+    }
+    tot[part][el] = s;
+    __syncthreads();
+    double run = e < E2 ? work_in[e] : 0.0;
+    for (int p = 0; p < part; ++p) run += tot[p][el];
+    if (e >= E2) return;
+    for (int c = c0; c < c1; c += 8) {
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = c + q < c1 ? sums[(int64_t)(c + q) * E2 + e] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (c + q < c1) {
+                pre[(int64_t)(c + q) * E2 + e] = run;
+                run += v[q];
+            }
+    }
+}
+
 // The chunk's exclusive prefix (work_in + the sums of all earlier chunks, each
-// block summing them itself: no serial pass over the chunks), the inclusive
+// block summing them itself: no serial pass over the chunks; or pre[c] from
+// rpar_scan_prefix_kernel when there are many chunks), the inclusive
 // scan inside the chunk (LDS), then the compat energies of the chunk's
 // kScanChunk / 2 samples (transr/transr.cpp:26-35 on the accumulated vectors)
 // and the hinge (common/trainer.cpp:138-141).  The last chunk leaves the work
@@ -982,7 +1026,7 @@ static __attribute__((unused)) __global__ __launch_bounds__(256) void rpar_scan_
 template <typename T>
 __global__ __launch_bounds__(1024) void rpar_scan_energy_kernel(RParArgs a, RParBufs<T> bf, const double* sums,
                                                                 int32_t nchunks, const double* work_in,
-                                                                double* work_out) {
+                                                                double* work_out, const double* pre) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double* run_l = (double*)smem;  // [kScanChunk][2 n]
     const int c = blockIdx.x, n = a.n, ld = a.ld;
@@ -1008,7 +1052,7 @@ __global__ __launch_bounds__(1024) void rpar_scan_energy_kernel(RParArgs a, RPar
     // chunks instead of ten), combined in group order
     const int E2 = 2 * n, G = max(1, (int)blockDim.x / E2);
     double* part = run_l + kScanChunk * E2;  // [G][2 n]
-    if ((int)threadIdx.x < G * E2) {
+    if (!pre && (int)threadIdx.x < G * E2) {
         const int g = threadIdx.x / E2, e = threadIdx.x % E2;
         double s[4] = {0, 0, 0, 0};
         for (int q0 = g * 16; q0 < c; q0 += G * 16) {
@@ -1022,9 +1066,14 @@ __global__ __launch_bounds__(1024) void rpar_scan_energy_kernel(RParArgs a, RPar
     }
     __syncthreads();
     for (int e = threadIdx.x; e < 2 * n; e += blockDim.x) {
-        double pre = 0.0;
-        for (int g = 0; g < G; ++g) pre += part[g * E2 + e];
-        double run = work_in[e] + pre;
+        double run;
+        if (pre) {
+            run = pre[(int64_t)c * E2 + e];
+        } else {
+            double p = 0.0;
+            for (int g = 0; g < G; ++g) p += part[g * E2 + e];
+            run = work_in[e] + p;
+        }
         const int side = e / n, i = e % n;
         for (int64_t k = c0; k < c1; k += 16) {
             double v[16];

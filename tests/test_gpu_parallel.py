@@ -212,6 +212,15 @@ def test_transr_parallel_compat(dim, St, mfma, monkeypatch):
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=True, mfma=mfma)
 
 
+@pytest.mark.parametrize("dim,mfma", [(50, True), (100, True), (100, False)])
+def test_transr_parallel_compat_chunk_prefix(dim, mfma, monkeypatch):
+    """The compat scan's chunk prefix made once by rpar_scan_prefix_kernel (the
+    path of batches with more than kScanDirectMax chunks, K5), forced on the
+    tiny set: the same model within rounding."""
+    monkeypatch.setenv("KB2E_RPAR_SCAN_PREFIX", "1")
+    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=2 if dim > 64 else 8, compat=True, mfma=mfma)
+
+
 def _hub_dataset(ne=300, nr=6, count=4000, seed=5):
     """Entity 0 heads ~half the triples: its event segments run to hundreds of
     events a batch (pair_prev_long_kernel's LDS table path)."""
