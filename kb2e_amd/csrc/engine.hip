@@ -1687,7 +1687,7 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
                         q[3], q[7], q[0] ? (double)q[4] / (double)q[0] : 0.0, q[5]);
                 if (c->rpar_cons_wide && cons_chainw_pipelined(c->n))
                     fprintf(stderr, "rpar_cons pipelined wide chain phases (walker: prologue+K0, window list, walk, "
-                            "B1 wait, row stores+fold, B2 wait, drain, window flags, tail, write-back, -; helper: "
+                            "B1 wait, row stores+fold, B2 wait, drain, window flags, tail, write-back+records, -; helper: "
                             "debt+fold+B2, X tile, B1 wait; walker: row+V, sums+rounds+g, later rows):");
                 else if (c->rpar_cons_wide)
                     fprintf(stderr, "rpar_cons wide chain phases (prologue, window list, rows+barrier, P+Gram+B1, "

@@ -572,6 +572,134 @@ __global__ __launch_bounds__(kWideThreads) void transr_cons_chain_wide_kernel(RP
     }
 }
 
+// The pair records per relation (n <= 128): a workgroup per relation of the batch
+// stages its final matrix once, transposed, in LDS (Wt[i][j] = W[j][i]) and turns
+// every record of the relation into da = -lr W G -- the violators' slots (pflag)
+// of its active samples, found by a thread a sample, and (entity'[r], r) when
+// stamped.  transr_cons_da_wide_kernel below reads the whole matrix from L2 for
+// every record instead (K5: ~88k records a batch x 80 KB).  A wave a record, two
+// elements j = 2l, 2l + 1 a lane: 16-byte row-pair reads of Wt, G_i as broadcasts.
+constexpr int kDaRelThreads = 1024;
+
+// The records of relation r (its samples [p0, p0 + 2 ns) of the batch's keys) with
+// its final matrix transposed in LDS (Wt [n][LT], LT even >= n, columns past n
+// never read into results); gb: [NT / 64][LT] doubles, list: [4 NT] ints, wsum:
+// [NT / 64] ints.  Ends with a barrier.
+template <int NT>
+__device__ __forceinline__ void relation_records(const RParArgs& a, const RParBufs<double>& bf, int r, int p0,
+                                                 int ns, const double* Wt, int LT, double* gb, int* list,
+                                                 int* wsum) {
+    using T = double;
+    constexpr int NW = NT / 64;
+    const int n = a.n, ld = a.ld;
+    const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
+    const bool relrec = r < a.ne && bf.relpair_stamp[r] == bf.stamp;
+    const T lr = (T)a.lr;
+    for (int wq = 0; wq < ns; wq += NT) {
+        const int q = wq + tid;
+        int kk = -1;
+        uint32_t keep = 0;
+        if (q < ns) {
+            kk = a.kl.kk_of(a.keys[p0 + 2 * q]);
+            if (a.act[kk]) {
+                const uchar4 f = *(const uchar4*)(bf.pflag + (int64_t)kk * 4);
+                keep = (f.x ? 1u : 0u) | (f.y ? 2u : 0u) | (f.z ? 4u : 0u) | (f.w ? 8u : 0u);
+            }
+        }
+        const int cnt = __builtin_popcount(keep);
+        int x = cnt;
+#pragma unroll
+        for (int sh = 1; sh < kWave; sh <<= 1) {
+            const int y = __shfl_up(x, sh);
+            if (l >= sh) x += y;
+        }
+        if (l == kWave - 1) wsum[w] = x;
+        __syncthreads();
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            const int ws = wsum[k];
+            off += k < w ? ws : 0;
+            tot += ws;
+        }
+        {
+            int pos = off + x - cnt;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((keep >> k) & 1) list[pos++] = kk * 4 + k;
+        }
+        if (wq == 0 && relrec) {
+            if (tid == 0) list[tot] = -2;
+            ++tot;
+        }
+        __syncthreads();  // the list
+        for (int m = w; m < tot; m += NW) {
+            const int sl = list[m];
+            T* row = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
+            T g[2];
+            lane_pair_load(row, n, g);
+            T* gw = gb + w * LT;
+            lane_pair_store(gw, n, g);  // (this wave's row: in-order LDS, no barrier)
+            T d0[4] = {T(0), T(0), T(0), T(0)}, d1[4] = {T(0), T(0), T(0), T(0)};
+            const int jl = 2 * l < n ? 2 * l : 0;
+            int i = 0;
+            for (; i + 4 <= n; i += 4) {
+                double2 wv[4];
+                T gi[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    wv[u] = *(const double2*)(Wt + (i + u) * LT + jl);
+                    gi[u] = gw[i + u];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    d0[u] = fma(wv[u].x, gi[u], d0[u]);
+                    d1[u] = fma(wv[u].y, gi[u], d1[u]);
+                }
+            }
+            for (; i < n; ++i) {
+                const double2 wv = *(const double2*)(Wt + i * LT + jl);
+                d0[0] = fma(wv.x, gw[i], d0[0]);
+                d1[0] = fma(wv.y, gw[i], d1[0]);
+            }
+            const T out[2] = {-lr * ((d0[0] + d0[1]) + (d0[2] + d0[3])), -lr * ((d1[0] + d1[1]) + (d1[2] + d1[3]))};
+            lane_pair_store(row, n, out);
+        }
+        __syncthreads();  // the list is rebuilt by the next window
+    }
+}
+
+__host__ __device__ constexpr size_t da_rel_lds(int n) {
+    return sizeof(double) * ((size_t)n * ((n + 1) & ~1) + (size_t)(kDaRelThreads / 64) * ((n + 1) & ~1)) +
+           sizeof(int) * ((size_t)4 * kDaRelThreads + kDaRelThreads / 64 + 8);
+}
+
+// A workgroup per relation segment of the batch (no search: the grid runs over the
+// batch's segments), the final matrix staged once, transposed.
+static __attribute__((unused)) __global__ __launch_bounds__(kDaRelThreads) void transr_cons_da_rel_kernel(
+    RParArgs a, RParBufs<double> bf) {
+    using T = double;
+    const int s = a.rel_begin[a.batch] + blockIdx.x;
+    if (s >= a.batch_seg[a.batch + 1]) return;
+    const int r = a.seg_row[s] - a.ne;
+    const int n = a.n, ld = a.ld, LT = (n + 1) & ~1;
+    const int p0 = a.seg_start[s], ns = (a.seg_start[s + 1] - p0) / 2;
+    constexpr int NW = kDaRelThreads / 64;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* Wt = (T*)smem;                  // [n][LT]
+    T* gb = Wt + n * LT;               // [NW][LT] a wave's G row
+    int* list = (int*)(gb + NW * LT);  // [4 kDaRelThreads]
+    int* wsum = list + 4 * kDaRelThreads;
+    const T* Wg = bf.W + (int64_t)r * n * ld;
+#pragma unroll 4
+    for (int idx = threadIdx.x; idx < n * n; idx += kDaRelThreads) {
+        const int j = idx / n, i = idx % n;
+        Wt[i * LT + j] = Wg[(int64_t)j * ld + i];
+    }
+    __syncthreads();
+    relation_records<kDaRelThreads>(a, bf, r, p0, ns, Wt, LT, gb, list, wsum);
+}
+
 // The pair records for n <= 128: transr_cons_da_kernel with two elements a lane
 // (G_i, i = 2l, 2l + 1; da_j = sum_i W[j][i] G_i by interleaved wave sums).
 static __attribute__((unused)) __global__ __launch_bounds__(256) void transr_cons_da_wide_kernel(RParArgs a,

@@ -101,7 +101,7 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
     unsigned long long n_chunks = 0, n_vio = 0, n_rounds = 0, max_m = 0;
     // KB2E_RPAR_STATS: cycles on thread 0 (the walker; g_seq_stats 8..23, relations of
     // >= 200 chunks also 24..39): 0 prologue + K0, 1 window list, 2 walk, 3 B1 wait,
-    // 4 row stores + fold, 5 B2 wait, 6 drain, 7 window flags, 8 tail, 9 write-back;
+    // 4 row stores + fold, 5 B2 wait, 6 drain, 7 window flags, 8 tail, 9 write-back + records;
     // thread 64 (helper wave 1): 10 debt (W update + records; from its last tick: the
     // fold and B2 too), 11 X tile, 12 B1 wait; the walk's violators split into 13
     // (row to LDS + V), 14 (sums, rounds, g), 15 (later rows; phase 2 keeps the rest)
@@ -619,12 +619,24 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
         for (int k = 0; k < 2; ++k) bf.pflag[kl * 4 + 2 + k] = ((tkeep >> k) & 1) ? vflag[pos++] : 0;
     }
     tick(8);
-    // the relation's matrix back, from the fragments
+    // the relation's matrix back, from the fragments, and transposed into LDS (K0's
+    // space) for the pair records da = -lr W G, made here: the other relations' blocks
+    // finish long before the hottest chain, so their records cost no batch time
+    const int LT = (n + 1) & ~1;
+    static_assert(NC * LA >= NC * NC, "Wt fits K0's space");
+    static_assert(3 * R * LA >= (NT / 64) * NC, "a G row a wave fits the row slots");
+    static_assert(2 * kWPPairs >= 4 * NT, "the record list fits the pair lists");
+    __syncthreads();  // every walk done with K0
     if (own && col < n) {
 #pragma unroll
         for (int q = 0; q < KS; ++q)
-            if (4 * q + kq < n) bf.W[((int64_t)r * n + 4 * q + kq) * ld + col] = bW[q];
+            if (4 * q + kq < n) {
+                bf.W[((int64_t)r * n + 4 * q + kq) * ld + col] = bW[q];
+                K0[col * LT + 4 * q + kq] = bW[q];
+            }
     }
+    __syncthreads();
+    relation_records<NT>(a, bf, r, p0, ns, K0, LT, Abuf, pe, wsum);
     tick(9);
     if (bf.stats) {
         __syncthreads();

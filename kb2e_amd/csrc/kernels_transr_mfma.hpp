@@ -72,7 +72,8 @@ __device__ __forceinline__ void block_gemm(int MT, int NT, int K, FA A, FB B, FP
 
 // block_gemm over a K whose bound KP is a compile-time multiple of 16 (the NP
 // padding of an image): loads without runtime guards, MFMAs only below K4.
-template <typename T, int KP, class FA, class FB, class FP>
+// (D: the k-steps whose fragments are loaded ahead of their MFMAs)
+template <typename T, int KP, class FA, class FB, class FP, int D = 8>
 __device__ __forceinline__ void block_gemm_k(int MT, int NT, int K4, FA A, FB B, FP put) {
     using M = Mfma16<T>;
     const int l = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -81,17 +82,17 @@ __device__ __forceinline__ void block_gemm_k(int MT, int NT, int K4, FA A, FB B,
         typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
         const int ar = mb * 16 + (l & 15), bc = nb * 16 + (l & 15), kq = l >> 4;
 #pragma unroll
-        for (int kb = 0; kb < KP; kb += 32) {
-            T av[8], bv[8];
+        for (int kb = 0; kb < KP; kb += 4 * D) {
+            T av[D], bv[D];
 #pragma unroll
-            for (int s = 0; s < 8; ++s) {
+            for (int s = 0; s < D; ++s) {
                 const int k = kb + 4 * s + kq;
                 const bool ok = kb + 4 * s < KP;  // compile time
                 av[s] = ok ? A(ar, k) : T(0);
                 bv[s] = ok ? B(k, bc) : T(0);
             }
 #pragma unroll
-            for (int s = 0; s < 8; ++s)
+            for (int s = 0; s < D; ++s)
                 if (kb + 4 * s < K4) acc = M::mma(av[s], bv[s], acc);
         }
 #pragma unroll
@@ -104,12 +105,15 @@ __host__ __device__ constexpr int rm_ld(int n) { return rm_np(n) + 2; }
 __host__ __device__ constexpr int rm_up16(int v) { return (v + 15) & ~15; }
 __host__ __device__ constexpr int rm_k4(int n) { return (n + 3) & ~3; }
 
-// Tile kernel LDS (elements of T): W [NP][L] | V [MV][L] | P [MV][L] (PROJ) | X [UY][L] | D [UY][L] |
+// Tile kernel LDS (elements of T): V [MV][L] | P [MV][L] (PROJ) | X [UY][L] | D [UY][L] |
 // coef [UY] (GRAD) | int ids [MV], kk [St].  A projection-only launch needs no D, a
-// gradient-only one (compat) neither W, V nor P: smaller images, more workgroups per CU.
+// gradient-only one (compat) neither V nor P.  W_r is not staged: the MFMA B
+// fragments come from global memory (L2; a tile group reads the same matrix), so
+// the image is small enough for two or more workgroups a CU to overlap their
+// gathers and HBM latencies (K5: one 160 KiB workgroup a CU spent the phase waiting).
 template <typename T>
 __host__ __device__ constexpr size_t rmfma_tile_lds(int n, int St, bool proj = true, bool grad = true) {
-    return sizeof(T) * ((proj ? (size_t)rm_np(n) * rm_ld(n) + 2 * (size_t)rm_up16(4 * St) * rm_ld(n) : 0) +
+    return sizeof(T) * ((proj ? 2 * (size_t)rm_up16(4 * St) * rm_ld(n) : 0) +
                         (grad ? 2 : 1) * (size_t)rm_up16(2 * St) * rm_ld(n) + rm_up16(2 * St)) +
            sizeof(int) * ((size_t)rm_up16(4 * St) + St);
 }
@@ -184,21 +188,22 @@ __device__ __forceinline__ void matvec_t(const T* WT, int L, int n, const T* xl,
 // exit at once.  Sums regroup (partials of up to tgroup tiles instead of one):
 // rounding-level differences only.
 template <typename T, bool PROJ, bool GRAD, int kNB>
-__global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParBufs<T> bf) {
+__global__ __launch_bounds__(512, 4) void transr_tile_mfma_kernel(RParArgs a, RParBufs<T> bf) {  // 4 waves an EU: two workgroups a CU
     using M = Mfma16<T>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int t0 = a.tile_first[a.batch_seg[a.batch]] + blockIdx.x;
     if (t0 >= a.tile_first[a.batch_seg[a.batch + 1]]) return;
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = lane_id();
-    const int G = nw == 8 && a.tgroup > 1 ? a.tgroup : 1;  // the register partial needs eight waves
+    // (a projection-only launch has no partial to share: a tile a block, all in parallel;
+    // the register partial needs eight waves)
+    const int G = GRAD && nw == 8 && a.tgroup > 1 ? a.tgroup : 1;
     const RTile tl0 = a.tiles[t0];
     if (tl0.q % G != 0) return;  // another block runs this tile
     const int ntl = min(G, a.tile_first[tl0.seg + 1] - t0);
     constexpr int NP = 16 * kNB, L = NP + 2;  // kNB = rm_np(n) / 16, exactly
     const int n = a.n, ld = a.ld;
     const int MV = rm_up16(4 * a.St), UY = rm_up16(2 * a.St);
-    T* Wl = (T*)smem;
-    T* V = Wl + (PROJ ? NP * L : 0);
+    T* V = (T*)smem;
     T* P = V + (PROJ ? MV * L : 0);
     T* X = P + (PROJ ? MV * L : 0);
     T* D = X + UY * L;  // GRAD only
@@ -228,7 +233,6 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
             }
             ids[row] = e;
         }
-        if (PROJ && ti == 0) stage_matrix_padded<T, NP>(Wl, bf.W + (int64_t)r * n * ld, n, ld);
         for (int idx = threadIdx.x; idx < UY * L; idx += blockDim.x) {
             X[idx] = T(0);
             if (GRAD) D[idx] = T(0);
@@ -238,8 +242,11 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
         if (PROJ) {  // V rows 4q + {0,1,2,3} = h, t, h', t' of sample q (zeros past the data)
             gather_rows<T, NP>(V, ids, MV, bf.ent, n, ld);
             __syncthreads();
-            block_gemm_k<T, NP>(MV / 16, kNB, rm_k4(n), [&](int m, int k) { return V[m * L + k]; },
-                          [&](int k, int c) { return Wl[k * L + c]; }, [&](int m, int c, T v) { P[m * L + c] = v; });
+            const T* Wg = bf.W + (int64_t)r * n * ld;  // W_r: B fragments from global memory (L2)
+            auto va = [&](int m, int k) { return V[m * L + k]; };
+            auto wb = [&](int k, int c) { return k < n && c < n ? Wg[(int64_t)k * ld + c] : T(0); };
+            auto pput = [&](int m, int c, T v) { P[m * L + c] = v; };
+            block_gemm_k<T, NP, decltype(va), decltype(wb), decltype(pput), 4>(MV / 16, kNB, rm_k4(n), va, wb, pput);
             __syncthreads();
             // one wave per sample: energies, hinge, x, d (transr/trainer.cpp:147-164, transr/transr.cpp:26-35)
             for (int q = w; q < cnt; q += nw) {
@@ -308,10 +315,12 @@ __global__ __launch_bounds__(512) void transr_tile_mfma_kernel(RParArgs a, RParB
             }
             __syncthreads();
             // y = W x for every update (transr/trainer.cpp:168-169): Y = X W^T
-            block_gemm_k<T, NP>(UY / 16, kNB, rm_k4(n), [&](int m, int k) { return X[m * L + k]; },
-                          [&](int k, int c) { return Wl[c * L + k]; }, [&](int m, int c, T v) {
-                              if (m < 2 * cnt && c < n) bf.y[((int64_t)kks[m >> 1] * 2 + (m & 1)) * ld + c] = v;
-                          });
+            auto xa = [&](int m, int k) { return X[m * L + k]; };
+            auto wtb = [&](int k, int c) { return k < n && c < n ? Wg[(int64_t)c * ld + k] : T(0); };
+            auto yput = [&](int m, int c, T v) {
+                if (m < 2 * cnt && c < n) bf.y[((int64_t)kks[m >> 1] * 2 + (m & 1)) * ld + c] = v;
+            };
+            block_gemm_k<T, NP, decltype(xa), decltype(wtb), decltype(yput), 4>(UY / 16, kNB, rm_k4(n), xa, wtb, yput);
         }
         if (GRAD) {
             if (!PROJ) {  // compat: directions from phase A, hinge from the work-vector scan

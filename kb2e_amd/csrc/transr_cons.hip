@@ -131,6 +131,8 @@ void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, int grid, si
 bool cons_chainw_supported(int n) { return n >= 1 && n <= kWideMaxN; }
 
 size_t cons_chainw_setup(int n) {
+    HIPCHK(hipFuncSetAttribute((const void*)transr_cons_da_rel_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)da_rel_lds(n)));
     const bool wp = use_wpipe(n);
     const size_t lds = wp ? chainwp_lds(n) : chainw_lds(n);
     HIPCHK(hipFuncSetAttribute(wp ? chainwp_fn(n) : chainw_fn(n), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -149,8 +151,18 @@ void cons_chainw_launch(const RParArgs& a, const RParBufs<double>& bf, size_t ld
     // (the LDS size was chosen by cons_chainw_setup under the same switch)
     if (use_wpipe(a.n)) HIPCHK(hipLaunchKernel(chainwp_fn(a.n), dim3(grid), dim3(kWPThreads), args, lds, stream));
     else HIPCHK(hipLaunchKernel(chainw_fn(a.n), dim3(grid), dim3(kWideThreads), args, lds, stream));
-    const int da_grid = (int)(((int64_t)4 * a.B + a.nr + 3) / 4);  // a wave a record
-    HIPCHK(hipLaunchKernel((const void*)transr_cons_da_wide_kernel, dim3(da_grid), dim3(256), args, 0, stream));
+    // the pair records: a workgroup per relation, its final matrix staged once
+    // (KB2E_RPAR_DA=wave: a wave a record over the whole record array, W from L2; A/B)
+    const char* dv = getenv("KB2E_RPAR_DA");
+    if (use_wpipe(a.n)) {
+        // (the pipelined chain makes its relation's records itself)
+    } else if (dv && std::string(dv) == "wave") {
+        const int da_grid = (int)(((int64_t)4 * a.B + a.nr + 3) / 4);  // a wave a record
+        HIPCHK(hipLaunchKernel((const void*)transr_cons_da_wide_kernel, dim3(da_grid), dim3(256), args, 0, stream));
+    } else {
+        HIPCHK(hipLaunchKernel((const void*)transr_cons_da_rel_kernel, dim3(a.nr), dim3(kDaRelThreads), args,
+                               da_rel_lds(a.n), stream));
+    }
 }
 
 bool cons_wave_supported(int n) { return n >= 1 && n <= 64; }
