@@ -633,11 +633,18 @@ __device__ __forceinline__ void relation_records(const RParArgs& a, const RParBu
             ++tot;
         }
         __syncthreads();  // the list
-        for (int m = w; m < tot; m += NW) {
+        // a wave's records one after another, the next one's G row loaded while the
+        // current one is made (a hot relation holds hundreds a batch)
+        auto rec_row = [&](int m) {
             const int sl = list[m];
-            T* row = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
-            T g[2];
-            lane_pair_load(row, n, g);
+            return sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
+        };
+        T gn[2] = {T(0), T(0)};
+        if (w < tot) lane_pair_load(rec_row(w), n, gn);
+        for (int m = w; m < tot; m += NW) {
+            T* row = rec_row(m);
+            T g[2] = {gn[0], gn[1]};
+            if (m + NW < tot) lane_pair_load(rec_row(m + NW), n, gn);
             T* gw = gb + w * LT;
             lane_pair_store(gw, n, g);  // (this wave's row: in-order LDS, no barrier)
             T d0[4] = {T(0), T(0), T(0), T(0)}, d1[4] = {T(0), T(0), T(0), T(0)};
