@@ -105,8 +105,10 @@ __host__ __device__ constexpr int rm_ld(int n) { return rm_np(n) + 2; }
 __host__ __device__ constexpr int rm_up16(int v) { return (v + 15) & ~15; }
 __host__ __device__ constexpr int rm_k4(int n) { return (n + 3) & ~3; }
 
+constexpr int kTileGroupMax = 8;  // tiles a gradient block runs at most (KB2E_RPAR_TGROUP is capped here)
+
 // Tile kernel LDS (elements of T): V [MV][L] | P [MV][L] (PROJ) | X [UY][L] | D [UY][L] |
-// coef [UY] (GRAD) | int ids [MV], kk [St].  A projection-only launch needs no D, a
+// coef [UY] (GRAD) | int ids [MV], kk [kTileGroupMax St].  A projection-only launch needs no D, a
 // gradient-only one (compat) neither V nor P.  W_r is not staged: the MFMA B
 // fragments come from global memory (L2; a tile group reads the same matrix), so
 // the image is small enough for two or more workgroups a CU to overlap their
@@ -115,7 +117,7 @@ template <typename T>
 __host__ __device__ constexpr size_t rmfma_tile_lds(int n, int St, bool proj = true, bool grad = true) {
     return sizeof(T) * ((proj ? 2 * (size_t)rm_up16(4 * St) * rm_ld(n) : 0) +
                         (grad ? 2 : 1) * (size_t)rm_up16(2 * St) * rm_ld(n) + rm_up16(2 * St)) +
-           sizeof(int) * ((size_t)rm_up16(4 * St) + St);
+           sizeof(int) * ((size_t)rm_up16(4 * St) + kTileGroupMax * (size_t)St);
 }
 
 // transRNorm kernel LDS: W [NP][L] | K [NP][L] | A0 [PP][L] | PG, PG2 [PP + 1][L] | s0 [PP + 2] |
@@ -196,10 +198,13 @@ __global__ __launch_bounds__(512, 4) void transr_tile_mfma_kernel(RParArgs a, RP
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = lane_id();
     // (a projection-only launch has no partial to share: a tile a block, all in parallel;
     // the register partial needs eight waves)
-    const int G = GRAD && nw == 8 && a.tgroup > 1 ? a.tgroup : 1;
+    const int G = GRAD && nw == 8 && a.tgroup > 1 ? min(a.tgroup, kTileGroupMax) : 1;
     const RTile tl0 = a.tiles[t0];
     if (tl0.q % G != 0) return;  // another block runs this tile
     const int ntl = min(G, a.tile_first[tl0.seg + 1] - t0);
+    // the group's relation segment (its tiles are consecutive chunks of St samples)
+    const int sp0 = a.seg_start[tl0.seg], sns = (a.seg_start[tl0.seg + 1] - sp0) / 2;
+    const int r = a.seg_row[tl0.seg] - a.ne;
     constexpr int NP = 16 * kNB, L = NP + 2;  // kNB = rm_np(n) / 16, exactly
     const int n = a.n, ld = a.ld;
     const int MV = rm_up16(4 * a.St), UY = rm_up16(2 * a.St);
@@ -209,7 +214,13 @@ __global__ __launch_bounds__(512, 4) void transr_tile_mfma_kernel(RParArgs a, RP
     T* D = X + UY * L;  // GRAD only
     T* coef = D + (GRAD ? UY * L : 0);
     int* ids = (int*)(coef + UY);  // entity of every V row
-    int* kks = ids + MV;           // sample index of every tile sample
+    int* kks = ids + MV;           // sample index of every tile sample (!PROJ: of the group's tiles)
+    if (!PROJ) {  // the gradient-only launch needs the samples alone: the whole group's at once
+        for (int i = threadIdx.x; i < ntl * a.St; i += blockDim.x) {
+            const int f = tl0.q * a.St + i;
+            kks[i] = f < sns ? a.kl.kk_of(a.keys[sp0 + 2 * f]) : -1;
+        }
+    }
     // the group's matrix partial: wave w holds output tiles w, w + 8, ... of the kNB x kNB grid
     constexpr int kAcc = (kNB * kNB + 7) / 8;
     typename M::acc_t gacc[kAcc];
@@ -218,10 +229,11 @@ __global__ __launch_bounds__(512, 4) void transr_tile_mfma_kernel(RParArgs a, RP
     T dr[2] = {T(0), T(0)};  // wave 0: the relation-vector partial
     int nact = 0;
     for (int ti = 0; ti < ntl; ++ti) {
-        int r, e0, cnt;
-        tile_range(a, t0 + ti, r, e0, cnt);
+        const int fq = (tl0.q + ti) * a.St;  // (tile_range without its loads)
+        const int e0 = sp0 + 2 * fq, cnt = min(a.St, sns - fq);
+        const int* kt = PROJ ? kks : kks + ti * a.St;
         // samples of the tile: ids resolved by one thread each, then the rows gathered by all
-        for (int row = threadIdx.x; row < MV; row += blockDim.x) {
+        for (int row = threadIdx.x; PROJ && row < MV; row += blockDim.x) {
             const int q = row >> 2, which = row & 3;
             int e = -1;
             if (q < cnt) {
@@ -325,7 +337,7 @@ __global__ __launch_bounds__(512, 4) void transr_tile_mfma_kernel(RParArgs a, RP
         if (GRAD) {
             if (!PROJ) {  // compat: directions from phase A, hinge from the work-vector scan
                 for (int q = w; q < cnt; q += nw) {
-                    const int kk = kks[q];
+                    const int kk = kt[q];
                     const bool act = a.act[kk] != 0;
 #pragma unroll
                     for (int u = 0; u < 2; ++u) {
