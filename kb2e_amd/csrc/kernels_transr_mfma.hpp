@@ -237,11 +237,17 @@ __global__ __launch_bounds__(512, 4) void transr_tile_mfma_kernel(RParArgs a, RP
             const int q = row >> 2, which = row & 3;
             int e = -1;
             if (q < cnt) {
-                const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
-                if (which == 0) kks[q] = kk;
-                const int i0 = a.si[kk], jj = a.sj[kk];
-                const int h = a.heads[i0], tt = a.tails[i0];
-                e = which == 0 ? h : which == 1 ? tt : which == 2 ? (a.side[kk] ? h : jj) : (a.side[kk] ? jj : tt);
+                if (a.td_ent) {  // the epoch's tile descriptors (rtile_desc_kernel, side stream)
+                    const int64_t td = (int64_t)(t0 + ti) * 8 + q;
+                    if (which == 0) kks[q] = a.td_kk[td];
+                    e = a.td_ent[td * 4 + which];
+                } else {
+                    const int kk = a.kl.kk_of(a.keys[e0 + 2 * q]);
+                    if (which == 0) kks[q] = kk;
+                    const int i0 = a.si[kk], jj = a.sj[kk];
+                    const int h = a.heads[i0], tt = a.tails[i0];
+                    e = which == 0 ? h : which == 1 ? tt : which == 2 ? (a.side[kk] ? h : jj) : (a.side[kk] ? jj : tt);
+                }
             }
             ids[row] = e;
         }
