@@ -300,8 +300,13 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
             }
         }
         T sq = (x[0] * x[0] + x[1] * x[1]) + (x[2] * x[2] + x[3] * x[3]);
-#pragma unroll
-        for (int m = 1; m < 32; m <<= 1) sq += __shfl_xor(sq, m);
+        // the row's 32 lanes: quad perms, half-row and row mirrors (DPP), then the
+        // other row of the pair (the same sums as xor 1 .. 16)
+        sq += dpp_mov<0xB1>(sq);
+        sq += dpp_mov<0x4E>(sq);
+        sq += dpp_mov<0x141>(sq);
+        sq += dpp_mov<0x140>(sq);
+        sq += __shfl_xor(sq, 16);
         if ((tid & 31) == 0 && j < R) qpart[j] = j < cn ? sq : T(0);
     };
     // W_c's unit rows (transr/trainer.cpp:178-180) before the last update's pairs;

@@ -259,9 +259,11 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                 sq = fma(x[u], x[u], sq);
             }
         }
-        sq += __shfl_xor(sq, 1);
-        sq += __shfl_xor(sq, 2);
-        sq += __shfl_xor(sq, 4);
+        // the row's eight lanes: quad perms, then the half-row mirror (DPP, no LDS
+        // round trips; the same sums as xor 1, 2, 4)
+        sq += dpp_mov<0xB1>(sq);
+        sq += dpp_mov<0x4E>(sq);
+        sq += dpp_mov<0x141>(sq);
         if ((threadIdx.x & 7) == 0) {
             qpart[j] = j < cn ? sq : T(0);
             for (int v = 1; v < NB; ++v) qpart[v * R + j] = T(0);
