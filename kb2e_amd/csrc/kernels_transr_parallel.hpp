@@ -496,14 +496,16 @@ __device__ __forceinline__ void transr_rel_rows_wave(RParArgs a, RParBufs<T> bf,
 // l & 15 holding elements 4 (l & 15) .. + 3 -- so a relation takes ceil((n + 1) / 4)
 // waves instead of n + 1 (the per-relation loads are shared, four times fewer
 // latency chains).
-template <typename T, bool NORM>
+// E = 8: the same for n <= 128 (eight elements a lane, four partial rows in flight).
+template <typename T, bool NORM, int E = 4>
 __device__ __forceinline__ void transr_rel_rows4_wave(RParArgs a, RParBufs<T> bf, int gw) {
     using T2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
+    constexpr int E2 = E / 2, NQ = E == 4 ? 8 : 4;  // element pairs a lane, partial rows in flight
     const int n = a.n, ld = a.ld;
     const int RW = (n + 4) >> 2;  // waves per relation segment (rows 0 .. n)
     const int s = a.rel_begin[a.batch] + gw / RW;
     if (s >= a.batch_seg[a.batch + 1]) return;
-    const int l = lane_id(), e0 = 4 * (l & 15);
+    const int l = lane_id(), e0 = E * (l & 15);
     const int j = (gw % RW) * 4 + (l >> 4);  // this DPP row's table row (j == n: the relation vector)
     const bool jok = NORM ? j <= n : j < n;
     const int r = a.seg_row[s] - a.ne;
@@ -521,53 +523,58 @@ __device__ __forceinline__ void transr_rel_rows4_wave(RParArgs a, RParBufs<T> bf
     uint64_t any = 0;
     for (int base = u0; base < u1 && !any; base += kWave) any = flags(base);
     if (!any) return;
-    const bool p0 = jok && e0 < ld, p1 = jok && e0 + 2 < ld;  // the two element pairs of the lane
-    auto load4 = [&](const T* rp, T (&v)[4]) {
-        const T2 x = p0 ? *(const T2*)(rp + e0) : T2{T(0), T(0)};
-        const T2 y = p1 ? *(const T2*)(rp + e0 + 2) : T2{T(0), T(0)};
-        v[0] = x.x;
-        v[1] = x.y;
-        v[2] = y.x;
-        v[3] = y.y;
+    bool pk[E2];  // the element pairs of the lane
+#pragma unroll
+    for (int k = 0; k < E2; ++k) pk[k] = jok && e0 + 2 * k < ld;
+    auto load4 = [&](const T* rp, T (&v)[E]) {
+#pragma unroll
+        for (int k = 0; k < E2; ++k) {
+            const T2 x = pk[k] ? *(const T2*)(rp + e0 + 2 * k) : T2{T(0), T(0)};
+            v[2 * k] = x.x;
+            v[2 * k + 1] = x.y;
+        }
     };
     const int jr = jok ? j : 0;
     T* row = jr < n ? bf.W + ((int64_t)r * n + jr) * ld : bf.rel + (int64_t)r * ld;
-    T v[4];
+    T v[E];
     load4(row, v);
     for (int base = u0; base < u1; base += kWave) {
         // the GRAD step's zero partials (inactive tiles) and the matrix-core transRNorm
         // step's unflagged ones are skipped; the VALU transRNorm step writes one for
         // every tile (a relation's first tile carries (entity[r], r) even when inactive)
         uint64_t m = (NORM || sel) ? flags(base) : (uint64_t)__ballot(base + l < u1);
-        while (m) {  // eight partial rows in flight, summed in slot order
-            T p[8][4];
-            bool use[8];
+        while (m) {  // NQ partial rows in flight, summed in slot order
+            T p[NQ][E];
+            bool use[NQ];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
+            for (int q = 0; q < NQ; ++q) {
                 use[q] = m != 0;
                 const int64_t lt = use[q] ? base + __builtin_ctzll(m) - ub : 0;
                 m &= m - 1;
                 if (use[q]) load4(jr < n ? bf.wpart + (lt * n + jr) * ld : bf.rpart + lt * ld, p[q]);
             }
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
+            for (int q = 0; q < NQ; ++q)
                 if (use[q])
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) v[k] += p[q][k];
+                    for (int k = 0; k < E; ++k) v[k] += p[q][k];
         }
     }
     if (NORM) {  // common::norm(v, false): unit length (padding elements are zero)
         T ss = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
+#pragma unroll
+        for (int k = 4; k < E; k += 4) ss += (v[k] * v[k] + v[k + 1] * v[k + 1]) + (v[k + 2] * v[k + 2] + v[k + 3] * v[k + 3]);
         ss += dpp_ror<8>(ss);
         ss += dpp_ror<4>(ss);
         ss += dpp_ror<2>(ss);
         ss += dpp_ror<1>(ss);
         const T len = sqrt(ss);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = v[k] / len;
+        for (int k = 0; k < E; ++k) v[k] = v[k] / len;
     }
-    if (p0) *(T2*)(row + e0) = T2{v[0], v[1]};
-    if (p1) *(T2*)(row + e0 + 2) = T2{v[2], v[3]};
+#pragma unroll
+    for (int k = 0; k < E2; ++k)
+        if (pk[k]) *(T2*)(row + e0 + 2 * k) = T2{v[2 * k], v[2 * k + 1]};
 }
 
 template <typename T, bool NORM>
@@ -575,9 +582,9 @@ __global__ __launch_bounds__(256) void transr_rel_rows_kernel(RParArgs a, RParBu
     transr_rel_rows_wave<T, NORM>(a, bf, (blockIdx.x * blockDim.x + threadIdx.x) >> 6);
 }
 
-template <typename T, bool NORM>
+template <typename T, bool NORM, int E = 4>
 __global__ __launch_bounds__(256) void transr_rel_rows4_kernel(RParArgs a, RParBufs<T> bf) {
-    transr_rel_rows4_wave<T, NORM>(a, bf, (blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    transr_rel_rows4_wave<T, NORM, E>(a, bf, (blockIdx.x * blockDim.x + threadIdx.x) >> 6);
 }
 
 // transRNorm (transr/trainer.cpp:35-64) per tile, on W'_r and the entity rows
@@ -936,12 +943,15 @@ __global__ __launch_bounds__(1024) void transr_entity_kernel(RParArgs a, RParBuf
 
 // Both row passes of one step in one launch (they touch disjoint tables):
 // workgroups [0, egrid) the entity rows, the rest one wave per (relation, row).
-template <typename T, bool PASS1, bool ROWS4>
+// RM: the relation-row layout -- 0 a row a wave, 4 / 8 four rows a wave with 4 / 8
+// elements a lane (n <= 64 / n <= 128)
+template <typename T, bool PASS1, int RM>
 __global__ __launch_bounds__(1024) void transr_rows_kernel(RParArgs a, RParBufs<T> bf, int32_t long_min,
                                                            int32_t egrid) {
     const int gw = (((int)blockIdx.x - egrid) * (int)blockDim.x + (int)threadIdx.x) >> 6;
     if ((int)blockIdx.x < egrid) transr_entity_block<T, PASS1>(a, bf, long_min, blockIdx.x, egrid);
-    else if (ROWS4) transr_rel_rows4_wave<T, PASS1>(a, bf, gw);
+    else if (RM == 4) transr_rel_rows4_wave<T, PASS1, 4>(a, bf, gw);
+    else if (RM == 8) transr_rel_rows4_wave<T, PASS1, 8>(a, bf, gw);
     else transr_rel_rows_wave<T, PASS1>(a, bf, gw);
 }
 
