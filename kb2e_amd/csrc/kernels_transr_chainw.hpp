@@ -583,8 +583,8 @@ constexpr int kDaRelThreads = 1024;
 
 // The records of relation r (its samples [p0, p0 + 2 ns) of the batch's keys) with
 // its final matrix transposed in LDS (Wt [n][LT], LT even >= n, columns past n
-// never read into results); gb: [NT / 64][LT] doubles, list: [4 NT] ints, wsum:
-// [NT / 64] ints.  Ends with a barrier.
+// never read into results); gb: [NT / 64][LT] doubles, list: [4 NT + 1] ints (the
+// window's slots and the relation record), wsum: [NT / 64] ints.  Ends with a barrier.
 template <int NT>
 __device__ __forceinline__ void relation_records(const RParArgs& a, const RParBufs<double>& bf, int r, int p0,
                                                  int ns, const double* Wt, int LT, double* gb, int* list,
@@ -678,7 +678,7 @@ __device__ __forceinline__ void relation_records(const RParArgs& a, const RParBu
 
 __host__ __device__ constexpr size_t da_rel_lds(int n) {
     return sizeof(double) * ((size_t)n * ((n + 1) & ~1) + (size_t)(kDaRelThreads / 64) * ((n + 1) & ~1)) +
-           sizeof(int) * ((size_t)4 * kDaRelThreads + kDaRelThreads / 64 + 8);
+           sizeof(int) * ((size_t)4 * kDaRelThreads + 1 + kDaRelThreads / 64 + 8);
 }
 
 // A workgroup per relation segment of the batch (no search: the grid runs over the
@@ -695,8 +695,8 @@ static __attribute__((unused)) __global__ __launch_bounds__(kDaRelThreads) void 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* Wt = (T*)smem;                  // [n][LT]
     T* gb = Wt + n * LT;               // [NW][LT] a wave's G row
-    int* list = (int*)(gb + NW * LT);  // [4 kDaRelThreads]
-    int* wsum = list + 4 * kDaRelThreads;
+    int* list = (int*)(gb + NW * LT);  // [4 kDaRelThreads + 1]
+    int* wsum = list + 4 * kDaRelThreads + 1;
     const T* Wg = bf.W + (int64_t)r * n * ld;
 #pragma unroll 4
     for (int idx = threadIdx.x; idx < n * n; idx += kDaRelThreads) {

@@ -630,7 +630,7 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
     const int LT = (n + 1) & ~1;
     static_assert(NC * LA >= NC * NC, "Wt fits K0's space");
     static_assert(3 * R * LA >= (NT / 64) * NC, "a G row a wave fits the row slots");
-    static_assert(2 * kWPPairs >= 4 * NT, "the record list fits the pair lists");
+    static_assert(2 * kWPPairs + 2 * R >= 4 * NT + 1, "the record list fits the pair lists (and the violator lists)");
     __syncthreads();  // every walk done with K0
     if (own && col < n) {
 #pragma unroll
