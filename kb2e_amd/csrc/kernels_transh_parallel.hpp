@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256) void transh_orth_check_kernel(HParArgs<T> a) {
 constexpr int kOrthWords = 4;  // 8-byte flag words per lane per pass
 // flagged samples of the previous batch from which normOrth takes the relation pass
 // (KB2E_HPAR_ORTH_MIN; oracle/parallel.py ORTH_REL_MIN)
-constexpr uint32_t kOrthRelMin = 256;
+constexpr uint32_t kOrthRelMin = 64;
 
 // Rows stored by this wave and not yet drained: a load of one of them waits
 // for the stores first (s_waitcnt vmcnt(0)); everything else loads at once.

@@ -361,7 +361,7 @@ def transh_orth_order(samples, flags, ids, r):
     return out
 
 
-ORTH_REL_MIN = 256  # kernels_transh_parallel.hpp kOrthRelMin
+ORTH_REL_MIN = 64  # kernels_transh_parallel.hpp kOrthRelMin
 
 
 def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, rate, margin=1.0, state=None,
