@@ -605,7 +605,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
     __syncthreads();
     if (mine && col < n)
         for (int jj = 0; jj < n; ++jj) bf.W[((int64_t)r * n + jj) * ld + col] = Wc[jj * L + col];
-    chain_records<T, NP, L>(a, bf, r, vio, nvt, Wc, Pbuf);
+    chain_records<T, NP, L>(a, bf, r, vio, nvt, Wc, Pbuf, 2 * R * L);
     if (bf.stats) {
         if (threadIdx.x == 0) {
             const unsigned long long cyc = (unsigned long long)(clock64() - ck0);

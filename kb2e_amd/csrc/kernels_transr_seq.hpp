@@ -156,21 +156,46 @@ __device__ __forceinline__ bool chain_first_tile(const RParArgs& a, int t0, int 
 // The relation's pair records G -> da = -lr W G with its final matrix
 // (transr/trainer.cpp:59-60; first order in lr the same as the matrix at the
 // pair's chunk), at the end of its chain: the nvt violator slots in vio (written
-// during the chain), W_c in LDS (stride L), `stage` [4][L] free LDS.  A wave a
+// during the chain), W_c in LDS (stride L), `stage` (stage_cap doubles) free LDS: [4][L] rows, then the slot list.  A wave a
 // record: the G row staged in LDS, lane j makes da_j = sum_i W[j][i] G_i (four
 // chains).  (Made here, the records of the ~440 relations that finish early
 // overlap the hottest relation's chain instead of following it in a kernel of
 // their own.)
 template <typename T, int NP, int L>
 __device__ __forceinline__ void chain_records(const RParArgs& a, const RParBufs<T>& bf, int r, const int32_t* vio,
-                                              int nvt, const T* Wc, T* stage) {
+                                              int nvt, const T* Wc, T* stage, int stage_cap) {
     const int n = a.n, ld = a.ld, w = threadIdx.x >> 6, l = lane_id();
-    T* gs = stage + w * L;
     const int nw = blockDim.x >> 6;
+    T* gs = stage + w * L;
+    // the violator slots in LDS when they fit (after the waves' staged rows), so a
+    // record's G row load waits on no global slot load; the rows prefetched PF
+    // records ahead (a hot relation has ~150 records a batch: ~40 a wave)
+    int* sl_l = (int*)(stage + nw * L);
+    const bool lds_sl = nvt <= 2 * (stage_cap - nw * L);
+    if (lds_sl) {
+        for (int i = threadIdx.x; i < nvt; i += blockDim.x) sl_l[i] = vio[i];
+        __syncthreads();
+    }
+    auto row_of = [&](int k) {
+        const int sl = lds_sl ? sl_l[k] : vio[k];
+        return sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
+    };
+    constexpr int PF = 4;
+    T pre[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+        const int k = w + p * nw;
+        pre[p] = k < nvt && l < n ? row_of(k)[l] : T(0);
+    }
     for (int k = w; k < nvt; k += nw) {
-        const int sl = vio[k];
-        T* row = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
-        if (l < NP) gs[l] = l < n ? row[l] : T(0);
+        T* row = row_of(k);
+        if (l < NP) gs[l] = pre[0];
+#pragma unroll
+        for (int p = 0; p + 1 < PF; ++p) pre[p] = pre[p + 1];
+        {
+            const int kn = k + PF * nw;
+            pre[PF - 1] = kn < nvt && l < n ? row_of(kn)[l] : T(0);
+        }
         wave_lds_sync();
         T acc[4] = {T(0), T(0), T(0), T(0)};
         const int j = l < NP ? l : 0;
@@ -614,7 +639,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
     if (mine && col < n)
         for (int jj = 0; jj < n; ++jj) bf.W[((int64_t)r * n + jj) * ld + col] = Wc[jj * L + col];
     __syncthreads();  // (the last records written; P free)
-    chain_records<T, NP, L>(a, bf, r, vio, nvt, Wc, P);
+    chain_records<T, NP, L>(a, bf, r, vio, nvt, Wc, P, R * L);
     if (bf.stats) {
         if (threadIdx.x == 0) {
             const unsigned long long cyc = (unsigned long long)(clock64() - ck0);
