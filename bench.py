@@ -341,6 +341,23 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
             run(late * batches - run.pos)
         eng.synchronize()
         late_s = timed(batches)
+    comm = None
+    if merger is not None:
+        # what the communicator saw, per rank (kb2e_comm_info for the in-engine RCCL
+        # merge; torch.distributed's view for the gloo merger) and the rank's device
+        import torch
+
+        if type(merger).__name__ == "NativeMerger":
+            nr, rk, first, cnt = eng.comm_info()
+        else:
+            nr, rk, first, cnt = dist.get_world_size(), dist.get_rank(), -1, -1
+        dev = torch.cuda.current_device()
+        bus = getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", -1)
+        row = torch.zeros((world, 6), dtype=torch.float64, device="cuda")
+        row[rank] = torch.tensor([nr, rk, first, cnt, dev, bus], dtype=torch.float64)
+        dist.all_reduce(row, op=dist.ReduceOp.SUM)
+        comm = [{"rank": int(x[1]), "comm_nranks": int(x[0]), "entity_block": [int(x[2]), int(x[3])],
+                 "device": int(x[4]), "pci_bus_id": int(x[5])} for x in row.tolist()]
     eng.close()
     samples = steps * B
     if dist is not None:
@@ -400,7 +417,7 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
     merge_rec = None
     if merger is not None:  # the epoch merge's share of the timed region (max over ranks)
         merge_rec = {"merges": merges, "ms_per_merge": merge_s / merges * 1e3 if merges else None,
-                     "share_of_timed": merge_s / elapsed, "kind": type(merger).__name__}
+                     "share_of_timed": merge_s / elapsed, "kind": type(merger).__name__, "ranks": comm}
     return {
         "value": samples / elapsed, "ms_per_step": elapsed / steps * 1e3, "B": B, "batches": batches,
         "merge": merge_rec, "device_bytes_per_gpu": device_bytes,
@@ -409,6 +426,9 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
         "active_fraction": a,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     # the PMC bytes over the same live launch time: the physical HBM rate
+                     "traffic_GBs": traffic / (avg_ms * 1e-3) / 1e9 if traffic and avg_ms > 0 else None,
+                     "traffic_frac": traffic / (avg_ms * 1e-3) / 1e9 / PEAK_HBM_GBS if traffic and avg_ms > 0 else None,
                      "kernel": dominant,
                      "kernel_avg_us": avg_ms * 1e3, "algorithmic_bytes_per_launch": bytes_per_launch,
                      "kernels_avg_us": kernels_us, "step_achieved_GBs": per_sample * samples / elapsed / 1e9},

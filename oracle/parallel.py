@@ -440,6 +440,8 @@ def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
         else:
             order = [(kk, q) for kk, fl in zip(a, flags) for q in fl]
         state["orth_flagged"] = sum(1 for fl in flags if fl)
+        if "flag_hist" in state:  # tests: the per-batch counts the gate saw
+            state["flag_hist"].append(state["orth_flagged"])
         for kk, q in order:
             rows = [(rel, r[kk]), (ent, h[kk]), (ent, t[kk]), None, (ent, nh[kk]), (ent, nt[kk])]
             tab, row = rows[q]

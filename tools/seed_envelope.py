@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--seed-epochs", type=int, default=500)
     ap.add_argument("--test", type=int, default=0, help="test triples scored (0 = all)")
     ap.add_argument("--compat", type=int, default=1)
+    ap.add_argument("--batches", type=int, default=100, help="batches an epoch (the reference's --batches)")
     ap.add_argument("--seeds", default="7,8,9")
     ap.add_argument("--schedules", default="ordered,parallel")
     ap.add_argument("--out", required=True)
@@ -127,10 +128,10 @@ def main():
         seed_tables = None
         if args.model == "R":
             seed_tables = transe_seed(ds, dim, args.seed_epochs, seed=seed)
-        row = {"seed": seed, "model": args.model, "dim": dim, "epochs": args.epochs,
+        row = {"seed": seed, "model": args.model, "dim": dim, "epochs": args.epochs, "batches": args.batches,
                "seed_epochs": args.seed_epochs, "transr_compat": bool(args.compat), "test": int(len(test))}
         for s in schedules:
-            r = train_and_evaluate(ds, args.model, dim, s, args.epochs, test=test, seed=seed,
+            r = train_and_evaluate(ds, args.model, dim, s, args.epochs, test=test, seed=seed, batches=args.batches,
                                    transr_compat=bool(args.compat), seed_tables=seed_tables, log=log)
             ls = [x[1] for x in r["losses"]]
             r["final_loss"] = ls[-1]
