@@ -98,7 +98,10 @@ const char* kb2e_last_error(const kb2e_ctx* ctx);
  * the Bernoulli table on the device.  Contexts take dim <= 512 for evaluation
  * and the table calls; training has narrower limits, checked here:
  * KB2E_EUNSUPPORTED for ORDERED TransR above dim 138 (FP64) / 195 (FP32), the
- * relation owner's matrix in LDS (PARALLEL TransR: dim <= 128 at kb2e_create). */
+ * relation owner's matrix in LDS.  PARALLEL TransR is checked at kb2e_create:
+ * its pair-by-pair transRNorm runs in FP64 up to dim 112 (KB2E_EUNSUPPORTED
+ * above it and in FP32, unless KB2E_RPAR_CONS=jacobi asks for the Jacobi form,
+ * up to dim 128). */
 kb2e_status kb2e_upload_triples(kb2e_ctx* ctx, const int32_t* heads, const int32_t* tails,
                                 const int32_t* relations, int64_t count);
 

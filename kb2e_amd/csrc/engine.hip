@@ -332,6 +332,8 @@ kb2e_status guarded(kb2e_ctx* c, F&& f) {
         return f();
     } catch (const HipError& e) {
         return fail(c, KB2E_EDEVICE, e.what());
+    } catch (const Unsupported& e) {
+        return fail(c, KB2E_EUNSUPPORTED, e.what());
     } catch (const std::invalid_argument& e) {
         return fail(c, KB2E_EINVAL, e.what());
     } catch (const std::bad_alloc&) {

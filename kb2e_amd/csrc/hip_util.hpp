@@ -13,6 +13,10 @@ namespace kb2e {
 struct HipError : std::runtime_error {
     using std::runtime_error::runtime_error;
 };
+// a configuration the engine does not run (KB2E_EUNSUPPORTED)
+struct Unsupported : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
 
 #define HIPCHK(expr)                                                                              \
     do {                                                                                          \

@@ -249,6 +249,14 @@ struct PendingRows {
     }
 };
 
+// Two sweeps in the order of the two-pass model: first the pairs only their own
+// relation touches (the relation row, entity rows flagged under it alone), then
+// the entity rows several relations flagged.  When transh_orth_rel_kernel ran, it
+// has done the first sweep's pairs and cleared their bits; when the gate skipped
+// it, this wave does them, in sample order -- the same result bit for bit, since
+// the relations' own pairs touch disjoint rows and normals (their interleaving
+// does not matter, only each relation's sample order).  So the gate on the
+// previous batch's flagged count (kOrthRelMin) is a schedule choice only.
 template <typename T, int CH>
 __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
     __shared__ int list[8 * kWave * kOrthWords];
@@ -256,6 +264,7 @@ __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
     RowReg<T, CH> W;
     int wid = -1;
     PendingRows pend;
+    for (int sweep = 0; sweep < 2; ++sweep)
     for (int base = 0; base < a.B; base += 8 * kWave * kOrthWords) {
         uint64_t word[kOrthWords];
 #pragma unroll
@@ -294,10 +303,17 @@ __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
                 r = a.rels[i0];
                 nh = sd ? h : j;
                 nt = sd ? j : t;
+                const int eid[6] = {r, h, t, r, nh, nt};
+                uint32_t sh = 0;  // the entity rows several relations flagged (second sweep)
+#pragma unroll
+                for (int q = 1; q < 6; ++q)
+                    if (q != 3 && ((bits >> q) & 1) && orth_shared(a, eid[q])) sh |= 1u << q;
+                bits = sweep == 0 ? bits & (int)~sh : (int)sh;
             }
             const int ng = min(kWave, count - g);
             for (int e = 0; e < ng; ++e) {
                 const uint32_t eb = (uint32_t)readlane_i32(bits, e);
+                if (eb == 0) continue;  // (the other sweep's pairs)
                 const int er = readlane_i32(r, e);
                 const int ids[6] = {er, readlane_i32(h, e), readlane_i32(t, e), er, readlane_i32(nh, e),
                                     readlane_i32(nt, e)};

@@ -180,6 +180,7 @@ struct RParBufs {
     int32_t chain_tiles; // chain kernels: tiles a window (0: the prefix table's 256; tests force windows)
     int32_t* vio;        // n <= 64 chain kernels: [tiles][kCPairs] the violators' slots of the relation whose
                          // first tile it is (-2: (entity[r], r)); its pair records are made in-kernel
+    uint32_t* err;       // pipelined chain: a bounded in-workgroup wait timed out (the host fails loudly)
 };
 
 __host__ __device__ constexpr int rm_up16_host_dev(int v) { return (v + 15) & ~15; }

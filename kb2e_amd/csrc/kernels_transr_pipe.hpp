@@ -171,6 +171,11 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                 }
             }
         }
+        if (threadIdx.x == 0) {  // (every thread has read misc[3..6] above)
+            misc[5] = 0;   // helper-wave arrivals (helper_sync)
+            misc[6] = -1;  // the chunk whose walk is complete
+            misc[7] = -1;  // (chunk << 6) | violators published so far
+        }
         __syncthreads();  // the P buffers are free again
     }
     bool changed = false;
@@ -207,32 +212,123 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
 #pragma unroll
         for (int q = 0; q < 4; ++q) out[(rt * 16 + kq + 4 * q) * L + cb * 16 + l16] = acc[q];
     };
-    // rows of chunk [b, e) of the window: R NP / 256 elements a thread, in registers
-    constexpr int kRowsPer = R * NP / kChainThreads;
+    // rows of chunk [b, e) of the window: the helper waves stage them (R NP / 192
+    // elements a thread, in registers), so the walker never waits on them
+    constexpr int kHT = kChainThreads - kWave;
+    constexpr int kRowsPer = (R * NP + kHT - 1) / kHT;
+    static_assert(kRowsPer <= 32, "rows_ok bits");
+    const int ht = (int)threadIdx.x - kWave;  // helper thread (w > 0)
     T rows[kRowsPer];
     uint32_t rows_ok = 0;
     auto load_rows = [&](int b, int e) {
+        if (w == 0) return;
         int ent[kRowsPer];
 #pragma unroll
         for (int q = 0; q < kRowsPer; ++q) {
-            const int f = b + (threadIdx.x + q * kChainThreads) / NP;
+            const int f = b + (ht + q * kHT) / NP;
             ent[q] = pe[f < kPipeList ? f : kPipeList - 1];
         }
         rows_ok = 0;
 #pragma unroll
         for (int q = 0; q < kRowsPer; ++q) {
-            const int idx = threadIdx.x + q * kChainThreads;
+            const int idx = ht + q * kHT;
             const int k = idx / NP, j = idx % NP;
-            const bool ok = b + k < e && ent[q] >= 0 && j < n;
+            const bool ok = idx < R * NP && b + k < e && ent[q] >= 0 && j < n;
             rows[q] = bf.ent[ok ? (uint32_t)ent[q] * (uint32_t)ld + (uint32_t)j : 0u];
             rows_ok |= (ok ? 1u : 0u) << q;
         }
     };
     auto store_rows = [&](int slot) {
+        if (w == 0) return;
 #pragma unroll
         for (int q = 0; q < kRowsPer; ++q) {
-            const int idx = threadIdx.x + q * kChainThreads;
-            Abuf[slot * R * L + (idx / NP) * L + idx % NP] = ((rows_ok >> q) & 1) ? rows[q] : T(0);
+            const int idx = ht + q * kHT;
+            if (idx < R * NP) Abuf[slot * R * L + (idx / NP) * L + idx % NP] = ((rows_ok >> q) & 1) ? rows[q] : T(0);
+        }
+    };
+    // The helper waves meet (no s_barrier: the walker runs on): every helper has paid
+    // its debt and written its projection / Gram tiles.  Bounded; a timeout sets
+    // *bf.err (the host fails loudly) and gives up.
+    int hsync_target = 0;
+    auto helper_sync = [&]() {
+        hsync_target += kChainThreads / kWave - 1;
+        if (l == 0) __hip_atomic_fetch_add(&misc[5], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (uint32_t sp = 0;
+             __hip_atomic_load(&misc[5], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < hsync_target; ++sp) {
+            if (sp > (1u << 22)) {
+                if (l == 0) __hip_atomic_store(bf.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    };
+    // The next chunk's corrections P_n -= lr C[:, v] g_v, by the helper waves while
+    // the walker walks: each violator as soon as the walker publishes it (misc[7]:
+    // (chunk << 6) | count, after its G row and vl entry; misc[6] = chunk when the
+    // walk ends), so after the walk only its last violators remain.  Then the
+    // |p_j|^2 partials (qpart[0], the other slices' partials zero).  Sixteen threads a
+    // row (one DPP row), NP / 16 columns each, rows rs, rs + 12, rs + 24.  The same
+    // FMAs per element in the same order as correct_q.
+    auto correct_inc = [&](T* Pn, int cn, const T* Pc, const int* vl, int ck) {
+        constexpr int NE = NP / 16, NPS = (R + 11) / 12;
+        const int rs = ht >> 4, cb = (ht & 15) * NE;
+        T x[NPS][NE];
+#pragma unroll
+        for (int p = 0; p < NPS; ++p) {
+            const int j = rs + 12 * p;
+#pragma unroll
+            for (int u = 0; u < NE; ++u) x[p][u] = j < cn ? Pn[j * L + cb + u] : T(0);
+        }
+        int used = 0;
+        for (uint32_t sp = 0;; ++sp) {
+            const bool done = __hip_atomic_load(&misc[6], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == ck;
+            const int pw = __hip_atomic_load(&misc[7], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int avail = (pw >> 6) == ck ? (pw & 63) : 0;
+            for (; used < avail; ++used) {
+                const int v = vl[used];
+                T gv[NE];
+#pragma unroll
+                for (int u = 0; u < NE; ++u) gv[u] = Pc[v * L + cb + u];
+#pragma unroll
+                for (int p = 0; p < NPS; ++p) {
+                    const int j = rs + 12 * p;
+                    if (j < cn) {
+                        const T gl = -lr * Cx[j * LG + v];
+#pragma unroll
+                        for (int u = 0; u < NE; ++u) x[p][u] = fma(gl, gv[u], x[p][u]);
+                    }
+                }
+            }
+            if (done) break;
+            if (sp > (1u << 22)) {
+                if (l == 0) __hip_atomic_store(bf.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        T sq[NPS];
+#pragma unroll
+        for (int p = 0; p < NPS; ++p) {
+            const int j = rs + 12 * p;
+            sq[p] = T(0);
+            if (j < cn) {
+#pragma unroll
+                for (int u = 0; u < NE; ++u) {
+                    if (used) Pn[j * L + cb + u] = x[p][u];
+                    sq[p] = fma(x[p][u], x[p][u], sq[p]);
+                }
+            }
+        }
+        row16_sums<T, NPS>(sq);
+        if ((ht & 15) == 0) {
+#pragma unroll
+            for (int p = 0; p < NPS; ++p) {
+                const int j = rs + 12 * p;
+                if (j < R) {
+                    qpart[j] = j < cn ? sq[p] : T(0);
+                    for (int v = 1; v < NB; ++v) qpart[v * R + j] = T(0);
+                }
+            }
         }
     };
     // P_n -= lr C[:, vio] G over the chunk's nv violators (vl; G: their rows of
@@ -435,6 +531,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
             T* Gm = Gbuf + pc * R * LG;
             T* Gn = Gbuf + (pc ^ 1) * R * LG;
             int* vl = vlist + par * R;
+            const int ck = (int)n_chunks;  // the chunk's tag in the publish words (misc[6], misc[7])
             ++n_chunks;
             tick(1);
             if (w == 0) {
@@ -448,7 +545,9 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                     for (int v = 1; v < NB; ++v) q += qpart[v * R + j];
                 }
                 uint32_t vmask = 0;
+                int npub = 0;  // violators published to the helper waves (correct_inc)
                 if (__ballot(j < cc && q > T(1)) != 0) {
+                    const T aaj = Gm[j * LG + j];  // |a_j|^2 (the Gram diagonal), off the violators' path
                     const int c0 = (l >> 5) * NH;
                     T x[NH];  // row j, columns c0 .. c0 + NH - 1
 #pragma unroll
@@ -460,6 +559,10 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                         if (!cand) break;
                         const int v = __builtin_ctzll(cand);
                         const int c = l;  // column
+                        // the scalars known at the pick, ahead of V: |p_v|^2, 1 / |p_v|^2, |a_v|^2
+                        const T pp = readlane_f(q, v);
+                        const T rpp = T(1) / pp;
+                        const T aa = readlane_f(aaj, v);
                         // the violator's current row to LDS for the column-lane layout
                         if (j == v) {
 #pragma unroll
@@ -477,15 +580,14 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                         T s2[2] = {pv * Vc, Vc * Vc};
                         wave_sums<T, 2>(s2);
                         tick(8);
-                        const T pp = readlane_f(q, v);
-                        const T pV = s2[0], VV = s2[1], aa = Gm[v * LG + v];
+                        const T pV = s2[0], VV = s2[1];
                         const T pvd = pV + aa * pp, vvd = VV + T(2) * aa * pV + aa * aa * pp;
-                        const T kappa = pvd / pp;
+                        const T kappa = pvd * rpp;
                         const T w2t = vvd - kappa * pvd;
                         const T w2 = w2t > T(0) ? w2t : T(0);
                         const T rho = T(1) - eps * kappa;
                         T S0, S1;
-                        const int m = transr_rounds_violator(pp, w2, eps, rho, S0, S1);
+                        const int m = transr_rounds_violator4(pp, w2, eps, rho, S0, S1);
                         n_rounds += (unsigned long long)m;
                         max_m = max_m > (unsigned long long)m ? max_m : (unsigned long long)m;
                         const T cpf = T(2) * (S0 + eps * S1 * kappa), cvf = T(2) * eps * S1;
@@ -509,6 +611,13 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                             const T tot = pair_sum32(qh);  // lanes j and j + 32: the same bits
                             if (upd) q = tot;
                         }
+                        // publish v to the helper waves: its G row (above) and vl entry first
+                        if (l == 0) {
+                            vl[npub] = v;
+                            __hip_atomic_store(&misc[7], (ck << 6) | (npub + 1), __ATOMIC_RELEASE,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                        ++npub;
                         vmask |= 1u << v;
                         cursor = v + 1;
                         ++n_vio;
@@ -521,10 +630,10 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                     if (sl >= 0) bf.pflag[sl] = vio_l ? 1 : 0;
                     else if (vio_l) bf.relpair_stamp[r] = bf.stamp;
                 }
-                if (l < R && ((vmask >> l) & 1u)) vl[__builtin_popcount(vmask & ((1u << l) - 1u))] = l;
                 if (l == 0) {
-                    misc[1] = (int)vmask;
-                    misc[2] = __builtin_popcount(vmask);
+                    misc[1 + 2 * par] = (int)vmask;
+                    misc[2 + 2 * par] = npub;
+                    __hip_atomic_store(&misc[6], ck, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 tick(2);
             } else {
@@ -544,11 +653,22 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                         else gram_tile(An, A, (tl - ng) / crt, (tl - ng) % crt, Cx, LG);
                     }
                 }
+                // every helper past its debt (chunk k-1's A slot and G rows are free) and its
+                // tiles (P_n, the Gram matrices complete)
+                helper_sync();
+                // chunk k+2's rows into the slot chunk k-1 left, chunk k+3's in flight
+                if (nb2 < npairs || cn > 0) {
+                    store_rows(ka == 0 ? 2 : ka - 1);
+                    const int n3 = nb2 < npairs ? chunk_end(nb2) : nb2;
+                    load_rows(n3, n3 < npairs ? chunk_end(n3) : n3);
+                }
+                // chunk k's violators into P_{k+1} as the walker publishes them, then |p|^2
+                if (cn > 0) correct_inc(Pn, cn, P, vl, ck);
             }
-            __syncthreads();  // B1
+            __syncthreads();  // B1: the walk, the next chunk's corrected projections and |p|^2
             tick(3);
-            const uint32_t vmask = (uint32_t)misc[1];
-            const int nv = misc[2];
+            const uint32_t vmask = (uint32_t)misc[1 + 2 * par];
+            const int nv = misc[2 + 2 * par];
             // chunk k's debt passes to the helpers (paid at the next chunk, or below)
             pend_nv = nv;
             pend_par = par;
@@ -558,19 +678,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
             pend_nvt = nvt;
             nvt += nv;
             if (vmask) changed = true;
-            // chunk k+2's rows into the slot chunk k - 1 left (its debt is paid), chunk
-            // k+3's in flight
-            const int ka2 = ka == 0 ? 2 : ka - 1;
-            if (nb2 < npairs || cn > 0) {
-                store_rows(ka2);
-                const int n3 = nb2 < npairs ? chunk_end(nb2) : nb2;
-                load_rows(n3, n3 < npairs ? chunk_end(n3) : n3);
-            }
-            tick(12);
             const bool restart = nbase == tail_start && changed && cn > 0;  // the tail: afresh
-            if (cn > 0 && !restart) correct_q(Pn, cn, nv, P, vl);
-            tick(14);
-            __syncthreads();  // B2
             tick(6);
             if (restart) {
                 apply_pending();  // the matrix up to date before the rows' renorm

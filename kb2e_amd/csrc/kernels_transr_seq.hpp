@@ -135,6 +135,45 @@ __device__ __forceinline__ int transr_rounds_violator(T Q0, T w2, T eps, T rho, 
     return m;
 }
 
+// transr_rounds_violator with the first four rounds as straight-line code: the
+// powers rho^t are the loop's products (the same bits), the four tests are
+// independent, and S0 / S1 add the same terms in the same order (+0 where a round
+// does not run), so the results are bit-identical to the loop's.  A violator
+// runs 1-3 rounds almost always (r21 counters: 2.8 on average); more than four
+// continue in the loop.  Without the branches between rounds the tests overlap
+// (a dependent FP64 chain of ~6 instead of ~25).
+template <typename T>
+__device__ __forceinline__ int transr_rounds_violator4(T Q0, T w2, T eps, T rho, T& S0, T& S1) {
+    const T e2w = eps * eps * w2;
+    const T r1 = rho, r2 = r1 * rho, r3 = r2 * rho, r4 = r3 * rho;
+    const bool c1 = r1 * r1 * Q0 + e2w * T(1) * T(1) * T(1) * T(1) > T(1);
+    const bool c2 = c1 && r2 * r2 * Q0 + e2w * T(2) * T(2) * r1 * r1 > T(1);
+    const bool c3 = c2 && r3 * r3 * Q0 + e2w * T(3) * T(3) * r2 * r2 > T(1);
+    const bool c4 = c3 && r4 * r4 * Q0 + e2w * T(4) * T(4) * r3 * r3 > T(1);
+    S0 = T(1);
+    S1 = T(0);
+    S0 += c1 ? r1 : T(0);
+    S1 += c1 ? T(1) * T(1) : T(0);
+    S0 += c2 ? r2 : T(0);
+    S1 += c2 ? T(2) * r1 : T(0);
+    S0 += c3 ? r3 : T(0);
+    S1 += c3 ? T(3) * r2 : T(0);
+    S0 += c4 ? r4 : T(0);
+    S1 += c4 ? T(4) * r3 : T(0);
+    int m = 1 + (int)c1 + (int)c2 + (int)c3 + (int)c4;
+    if (c4) {  // (uniform: every lane holds the same scalars)
+        T rt = r4 * rho, rtm1 = r4;
+        while (m < kRParMaxIter && rt * rt * Q0 + e2w * (T)m * (T)m * rtm1 * rtm1 > T(1)) {
+            S0 += rt;
+            S1 += (T)m * rtm1;
+            rtm1 = rt;
+            rt *= rho;
+            ++m;
+        }
+    }
+    return m;
+}
+
 // The chain kernels' block -> relation map: block b takes the b-th most frequent
 // relation (a.rel_order), so the hot relations' long chains start first instead
 // of waiting for a dispatch slot behind short ones; its first tile g0 within the

@@ -377,11 +377,12 @@ def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
     relation row once per sample) runs the reference's normOrth
     (common/utils.cpp:79-111): first the pairs whose row only their relation
     touches (per relation, samples in order), then the entity rows flagged
-    under several relations (samples in order) -- when the previous batch
-    flagged at least `orth_rel_min` samples; otherwise every flagged pair in
-    sample order (the GPU's one-wave pass alone).  `state` carries the previous
-    batch's flagged-sample count across calls (the engine's, across epochs;
-    zero before the first batch).
+    under several relations (samples in order).  The GPU runs the first pass as a
+    wave per relation when the previous batch flagged at least `orth_rel_min`
+    samples and on its one wave otherwise, with the same result (the relations'
+    own pairs touch disjoint rows and normals), so the gate does not enter the
+    model; `state` carries the previous batch's flagged-sample count (the
+    engine's, across epochs) for the tests that check both kernels ran.
     """
     from oracle import orc
 
@@ -435,10 +436,11 @@ def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
             rows = [(rel, r[kk]), (ent, h[kk]), (ent, t[kk]), None, (ent, nh[kk]), (ent, nt[kk])]
             flags.append([q for q in range(6) if rows[q] is not None and W[r[kk]] @ rows[q][0][rows[q][1]] > 0.1])
         ids = {kk: (r[kk], h[kk], t[kk], None, nh[kk], nt[kk]) for kk in a}
-        if state.get("orth_flagged", 0) >= orth_rel_min:
-            order = transh_orth_order(list(a), flags, ids, r)
-        else:
-            order = [(kk, q) for kk, fl in zip(a, flags) for q in fl]
+        # the two-pass order whichever kernel runs it: the gate on the previous batch's
+        # flagged count (orth_rel_min) picks the relation pass or the one-wave pass's
+        # first sweep, which give the same result (kernels_transh_parallel.hpp
+        # transh_orth_fix_kernel); it is recorded for the tests, not applied
+        order = transh_orth_order(list(a), flags, ids, r)
         state["orth_flagged"] = sum(1 for fl in flags if fl)
         if "flag_hist" in state:  # tests: the per-batch counts the gate saw
             state["flag_hist"].append(state["orth_flagged"])

@@ -90,8 +90,9 @@ def _cons_form(dim, mfma):
     kernels_transr_chainw.hpp elsewhere -- unless
     KB2E_RPAR_CONS picks the Jacobi tile / wave kernels; Jacobi above 112."""
     ck = os.environ.get("KB2E_RPAR_CONS", "")
-    if ck in ("tile", "jacobi") or dim > 112:
+    if ck in ("tile", "jacobi"):
         return "jacobi"
+    assert dim <= 112, "PARALLEL TransR above n = 112 runs only on request (KB2E_RPAR_CONS=jacobi)"
     return "chunk1"
 
 
@@ -100,6 +101,8 @@ def _transr_vs_model(ds, dim, epochs, monkeypatch, *, St=8, compat=False, distan
     from oracle.parallel import transr_parallel_batches
     monkeypatch.setenv("KB2E_RPAR_ST", str(St))
     monkeypatch.setenv("KB2E_RPAR_MFMA", "1" if mfma else "0")
+    if dim > 112:  # the Jacobi transRNorm is the only form there, and only on request
+        monkeypatch.setenv("KB2E_RPAR_CONS", "jacobi")
     cons = _cons_form(dim, mfma)
     m = orc.Model("R", dim, ds.num_entities, ds.num_relations, rate=rate, distance=distance, batches=batches,
                   transr_compat=compat)
@@ -260,6 +263,20 @@ def test_transr_parallel_independent_of_tile_size(monkeypatch):
             assert max_abs(x, y) < 1e-12
 
 
+@pytest.mark.parametrize("dim,precision", [(120, 64), (50, 32)])
+def test_transr_parallel_refuses_without_chain(dim, precision, monkeypatch):
+    """PARALLEL TransR runs the pair-by-pair transRNorm (FP64, n <= 112); elsewhere
+    the context is refused (KB2E_EUNSUPPORTED) instead of silently taking the Jacobi
+    form, whose loss departs from the reference's -- unless asked for by name."""
+    from kb2e_amd.engine import EngineError
+    monkeypatch.delenv("KB2E_RPAR_CONS", raising=False)
+    ds = tiny()
+    with pytest.raises(EngineError, match="EUNSUPPORTED"):
+        Engine("R", dim, ds.num_entities, ds.num_relations, precision=precision, schedule="parallel")
+    monkeypatch.setenv("KB2E_RPAR_CONS", "jacobi")
+    Engine("R", dim, ds.num_entities, ds.num_relations, precision=precision, schedule="parallel").close()
+
+
 def test_transr_parallel_fp32_close(monkeypatch):
     """FP32 tables: hinge decisions flip at the margin, so statistics, not elements.
     (Both on the Jacobi transRNorm: the chunked chain is FP64 only.)"""
@@ -312,9 +329,9 @@ def test_transh_parallel(dim):
 @pytest.mark.parametrize("orth_min", [0, 1 << 30, 8])
 def test_transh_parallel_orth_gate(orth_min, monkeypatch):
     """normOrth's relation pass runs only when the previous batch flagged at least
-    KB2E_HPAR_ORTH_MIN samples (0: always; huge: never, every pair on the one-wave
-    pass in sample order; 8: batches of both kinds on the tiny set); the CPU
-    model applies the same rule."""
+    KB2E_HPAR_ORTH_MIN samples (0: always; huge: never, the one-wave pass takes
+    the relations' own pairs in its first sweep; 8: batches of both kinds on the
+    tiny set).  The result does not depend on it: one CPU model for all three."""
     monkeypatch.setenv("KB2E_HPAR_ORTH_MIN", str(orth_min))
     _transh_vs_model(tiny(), 20, 2, orth_min=orth_min)
 

@@ -12,6 +12,9 @@
 #   bash tools/gpu.sh hits     <tag>                        FB15k-shaped Hits@10 schedule parity, four configs
 #   bash tools/gpu.sh k5       <tag>                        n > 64 parity tests, K5 tests, the K5 line
 #   bash tools/gpu.sh final    <tag>                        suite + default line + K5 line
+#   bash tools/gpu.sh timeline <tag>                        kernel timeline of the driver-style line (K=20)
+# (ab: AB_EPOCH=1 also times the whole epoch and epoch 50, e.g. the TransH gate sweep
+#  AB_EPOCH=1 bash tools/gpu.sh ab gate transh_fb15k KB2E_HPAR_ORTH_MIN 0 16 64 256)
 set -o pipefail
 CMD=$1; TAG=${2:-$1}; shift 2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -45,8 +48,23 @@ case "$CMD" in
     CFG=$1; VAR=$2; shift 2
     for V in "$@"; do
       if [ "$V" = "-" ]; then unset "$VAR"; else export "$VAR=$V"; fi
-      bench_run "ab_${V}" 400 --config "$CFG" --only --no-cpu-baseline --no-epoch --steps 100 --warmup 100 || exit 1
+      if [ -n "$AB_EPOCH" ]; then EP="--late-epoch 50"; else EP="--no-epoch"; fi
+      bench_run "ab_${V}" 400 --config "$CFG" --only --no-cpu-baseline $EP --steps 100 --warmup 100 || exit 1
     done ;;
+  timeline)
+    timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/tl -o run --output-format csv -- \
+        python3 bench.py --only --no-cpu-baseline --no-epoch --steps 20 --warmup 5 > "$OUT/bench.log" 2>&1 || fail trace $? "$OUT/bench.log"
+    python3 - "$(find /tmp/tl -name "*kernel_trace.csv" | head -1)" > "$OUT/timeline.txt" <<'PY'
+import csv, sys
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+t0 = int(rows[max(0, len(rows) - 400)]["Start_Timestamp"])
+for r in rows:
+    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    if s >= t0:
+        n = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("kb2e::", "")[:56]
+        print(f"{(s - t0) / 1e3:10.1f} {(e - s) / 1e3:8.1f} q{r.get('Queue_Id', '?'):>3} {n}")
+PY
+    tail -5 "$OUT/timeline.txt" ;;
   profile)
     SCHED=$1; shift
     bench_run bench 400 --schedule "$SCHED" "$@" || exit 1

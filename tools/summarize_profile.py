@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a tools/gpu_profile.sh run into profiles/ (committed evidence).
+"""Summarise a tools/gpu.sh profile run into profiles/ (committed evidence).
 
 Writes profiles/<tag>_<config>_<schedule>_f<prec>.md (kernel stats table + PMC
 traffic) and profiles/pmc_<config>_<schedule>_f<prec>.json (HBM bytes per batch
@@ -126,7 +126,7 @@ def main(src, tag, config, prec, schedule="parallel", batches="200"):
         per_kernel["mfma_f64"] = mf
     out_json = os.path.join(root, "profiles", f"pmc_{config}_{schedule}_f{prec}.json")
     json.dump(per_kernel, open(out_json, "w"), indent=1, sort_keys=True)
-    lines = [f"# Profile {tag}: {config}, {schedule} schedule (f{prec})", "", "Command: `tools/gpu_profile.sh` on one MI355X "
+    lines = [f"# Profile {tag}: {config}, {schedule} schedule (f{prec})", "", "Command: `tools/gpu.sh profile` on one MI355X "
              "(rocprofv3 --kernel-trace --stats; separate --pmc FETCH_SIZE / WRITE_SIZE passes).", "",
              "## bench.py line", "", "```", bench, "```", "", "## Kernel stats (rocprofv3 --stats)", "",
              "| kernel | calls | total ms | avg us | % |", "|---|---|---|---|---|"]
