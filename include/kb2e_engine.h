@@ -95,13 +95,10 @@ const char* kb2e_last_error(const kb2e_ctx* ctx);
 /* Trainer::add for every training triple, in train-file order, plus the
  * per-relation head/tail co-occurrence means of Trainer::loadFiles
  * (common/trainer.cpp:26-32, 151-201).  Builds the negative-sample filter and
- * the Bernoulli table on the device.  Contexts take dim <= 512 for evaluation
- * and the table calls; training has narrower limits, checked here:
- * KB2E_EUNSUPPORTED for ORDERED TransR above dim 138 (FP64) / 195 (FP32), the
- * relation owner's matrix in LDS.  PARALLEL TransR is checked at kb2e_create:
- * its pair-by-pair transRNorm runs in FP64 up to dim 112 (KB2E_EUNSUPPORTED
- * above it and in FP32, unless KB2E_RPAR_CONS=jacobi asks for the Jacobi form,
- * up to dim 128). */
+ * the Bernoulli table on the device.  Contexts take dim <= 512 (ORDERED
+ * TransR above dim 137 keeps the relation owner's matrix in L2 instead of LDS);
+ * PARALLEL TransR trains dim <= 128, checked at kb2e_create
+ * (KB2E_EUNSUPPORTED above). */
 kb2e_status kb2e_upload_triples(kb2e_ctx* ctx, const int32_t* heads, const int32_t* tails,
                                 const int32_t* relations, int64_t count);
 

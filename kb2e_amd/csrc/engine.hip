@@ -169,6 +169,8 @@ struct kb2e_ctx {
     DevBuf rpar_vio;              // the n <= 64 chain kernels' violator slots (in-kernel pair records)
     bool rpar_cons_wide = false;  // the same chain for n <= 112 off the n <= 64 matrix-core path (kernels_transr_chainw.hpp)
     size_t rpar_wide_lds = 0;
+    bool rpar_cons_gen = false;   // the same chain for FP32 and 112 < n <= 128 (kernels_transr_chaing.hpp)
+    size_t rpar_gen_lds = 0;
     DevBuf rpar_pflag, rpar_cons_tile, rpar_cpairs, rpar_cnrows;
     DevBuf rpar_y, rpar_wpart, rpar_rpart, rpar_tile_act, rpar_pair, rpar_relpair, rpar_relpair_stamp, rpar_scan_pre, rpar_tiles,
         rpar_ntiles, rpar_tile_first, rpar_rel_begin, rpar_scan;
@@ -1295,12 +1297,6 @@ const char* kb2e_last_error(const kb2e_ctx* ctx) { return ctx ? ctx->err.c_str()
 kb2e_status kb2e_upload_triples(kb2e_ctx* c, const int32_t* h, const int32_t* t, const int32_t* r, int64_t count) {
     return guarded(c, [&] {
         if (!h || !t || !r || count < 1) return fail(c, KB2E_EINVAL, "empty triple set");
-        {  // ORDERED TransR training: the relation owner's matrix must fit in LDS (evaluation has no such limit)
-            const kb2e_config& g = c->cfg;
-            if (g.model == KB2E_TRANSR && g.schedule == KB2E_SCHEDULE_ORDERED &&
-                ((size_t)g.dim * (g.dim + 1) + 3 * (size_t)g.dim) * (g.precision / 8) > 152 * 1024)
-                return fail(c, KB2E_EUNSUPPORTED, "ORDERED TransR trains dim <= 138 (FP64) / 195 (FP32)");
-        }
         HIPCHK(hipSetDevice(c->cfg.device));
         c->ts.build(h, t, r, count, c->cfg.num_entities, c->cfg.num_relations);
         c->heads.alloc(count * 4);
@@ -1695,9 +1691,10 @@ kb2e_status kb2e_take_stats(kb2e_ctx* c, double* loss, int64_t* active) {
                     fprintf(stderr, "rpar_cons wide chain phases (prologue, window list, rows+barrier, P+Gram+B1, "
                             "K0, V+sums, B(1), rounds+g, B(2), later pairs, B(3), records+W update, chunk barrier, "
                             "window flags, tail, write-back):");
-                else
-                    fprintf(stderr, "rpar_cons chunk phases (prologue, issue+renorm, P+Gram+B1, K0, violators, B2, "
-                            "W update+rows+B3; violator: V, sums, rounds, record, update):");
+                else  // (the tick indices of kernels_transr_pipe.hpp; the serial kernel's differ, kernels_transr_seq.hpp)
+                    fprintf(stderr, "rpar_cons chunk phases (prologue, chunk start, walk end + publish, B1 wait, "
+                            "pick + row to LDS, helper B1 wait, after B1, V, sums, rounds + g, g store, later rows; helper wave 1: debt, tiles, "
+                            "helper_sync wait, rows + corrections):");
                 for (int k = 8; k < 24; ++k) fprintf(stderr, " %llu", q[k]);
                 fprintf(stderr, "; hot relations (%llu, %llu chunks, %llu violators):", q[41], q[40], q[42]);
                 for (int k = 24; k < 40; ++k) fprintf(stderr, " %llu", q[k]);

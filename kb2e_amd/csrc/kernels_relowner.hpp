@@ -947,12 +947,32 @@ __global__ __launch_bounds__(256) void transr_compat_energy_kernel(RScoreArgs<T>
 // with the relation matrix W (n x ldl) in LDS and `abuf` (n) as broadcast
 // scratch.  Sums over j run in the reference's order for the check; the
 // per-column dot products of the iteration use the wave reduction.
-template <typename T, int CH>
+// The owner's matrix W' in LDS, or (WG: dim too wide for the LDS, kb2e_upload_triples)
+// the relation's next-matrix row in global memory itself: one wave owns it, its
+// own stores are drained before a barrier and re-read past the L1 (sc1), the
+// convention of the entity rows handed between owners.
+template <bool WG, typename T>
+__device__ __forceinline__ T wld(const T* p) {
+    if constexpr (WG) return load_sc1(p);
+    else return *p;
+}
+template <bool WG, typename T>
+__device__ __forceinline__ void wst(T* p, T v) {
+    if constexpr (WG) store_sc1(p, v);
+    else *p = v;
+}
+template <bool WG>
+__device__ __forceinline__ void wsync() {
+    if constexpr (WG) drain_stores();
+    __syncthreads();
+}
+
+template <typename T, int CH, bool WG = false>
 __device__ void transr_norm(RowReg<T, CH>& A, T* Wl, int ldl, T* abuf, int n, T lr OWNER_PC_PARAM) {
     const int l = lane_id();
     for (int iter = 0; iter < 100000; ++iter) {
         A.store(abuf, n);
-        __syncthreads();
+        wsync<WG>();
         T xx = T(0);
 #pragma unroll
         for (int c = 0; c < CH; ++c)
@@ -961,7 +981,7 @@ __device__ void transr_norm(RowReg<T, CH>& A, T* Wl, int ldl, T* abuf, int n, T 
                 const int i = c * (kWave * kVec) + l * kVec + k;
                 if (i >= n) continue;
                 T tmp = T(0);
-                for (int j = 0; j < n; ++j) tmp += Wl[j * ldl + i] * abuf[j];
+                for (int j = 0; j < n; ++j) tmp += wld<WG>(Wl + (int64_t)j * ldl + i) * abuf[j];
                 xx += tmp * tmp;
             }
         xx = wave_sum(xx);
@@ -977,7 +997,7 @@ __device__ void transr_norm(RowReg<T, CH>& A, T* Wl, int ldl, T* abuf, int n, T 
 #pragma unroll
                 for (int k = 0; k < kVec; ++k) {
                     const int j = c * (kWave * kVec) + l * kVec + k;
-                    if (j < n) part += Wl[j * ldl + i] * A.v[c][k];
+                    if (j < n) part += wld<WG>(Wl + (int64_t)j * ldl + i) * A.v[c][k];
                 }
             T tmp = wave_sum(part);
             tmp *= T(2);
@@ -988,11 +1008,11 @@ __device__ void transr_norm(RowReg<T, CH>& A, T* Wl, int ldl, T* abuf, int n, T 
                 for (int k = 0; k < kVec; ++k) {
                     const int j = c * (kWave * kVec) + l * kVec + k;
                     if (j >= n) continue;
-                    const T wn = Wl[j * ldl + i] - coef * A.v[c][k];
-                    Wl[j * ldl + i] = wn;
+                    const T wn = wld<WG>(Wl + (int64_t)j * ldl + i) - coef * A.v[c][k];
+                    wst<WG>(Wl + (int64_t)j * ldl + i, wn);
                     A.v[c][k] = A.v[c][k] - coef * wn;
                 }
-            __syncthreads();
+            wsync<WG>();
         }
         OWNER_MARK(7);
     }
@@ -1014,16 +1034,17 @@ __device__ void w_fill(T* Wl, int ldl, const T* Wg, int n, int ld) {
     }
 }
 
-template <typename T, int CH>
+template <typename T, int CH, bool WG = false>
 __global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32_t stamp) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int seg = a.owner_seg[(int64_t)a.batch * a.owners + blockIdx.x];
     if (seg < 0) return;
     const int p0 = a.seg_start[seg], p1 = a.seg_start[seg + 1];
     const int n = a.n;
-    const int ldl = n + 1;
-    T* Wl = (T*)smem;                    // n x ldl: the owner's relation matrix (next)
-    T* abuf = Wl + n * ldl;              // n: broadcast scratch
+    const int ldl = WG ? a.ld : n + 1;
+    // n x ldl: the owner's relation matrix (next): in LDS, or (WG) the table row itself
+    T* Wl = WG ? nullptr : (T*)smem;
+    T* abuf = (T*)smem + (WG ? 0 : n * ldl);  // n: broadcast scratch
     T* xb = abuf + n;                    // n: update direction
     T* db = xb + n;                      // n: snapshot head - tail
     const int l = lane_id();
@@ -1039,12 +1060,13 @@ __global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32
         if (!a.act[kk]) continue;
         const UpdateIds d = decode_update(a, key, true);
         if (d.r != cur) {
-            __syncthreads();
+            wsync<WG>();
             if (cur >= 0) {
-                w_spill(Wl, ldl, a.w + (int64_t)cur * n * a.ld, n, a.ld);
+                if (!WG) w_spill(Wl, ldl, a.w + (int64_t)cur * n * a.ld, n, a.ld);
                 if (l == 0) a.wtouched[cur] = stamp;
             }
-            w_fill(Wl, ldl, a.w + (int64_t)d.r * n * a.ld, n, a.ld);
+            if (WG) Wl = a.w + (int64_t)d.r * n * a.ld;
+            else w_fill(Wl, ldl, a.w + (int64_t)d.r * n * a.ld, n, a.ld);
             cur = d.r;
             __syncthreads();
         }
@@ -1074,7 +1096,7 @@ __global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32
         // rank-1 update of W' (transr/trainer.cpp:167): W'[j][i] -= (blr x_i) d_j
         for (int idx = l; idx < n * n; idx += kWave) {
             const int j = idx / n, i = idx % n;
-            Wl[j * ldl + i] = Wl[j * ldl + i] - (blr * xb[i]) * db[j];
+            wst<WG>(Wl + (int64_t)j * ldl + i, wld<WG>(Wl + (int64_t)j * ldl + i) - (blr * xb[i]) * db[j]);
         }
         OWNER_MARK(3);
         // entity deltas with the snapshot matrix, summed over i in order (:168-169)
@@ -1116,18 +1138,22 @@ __global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32
         R.norm(n, false);
         E[0].norm(n, false);
         E[tslot].norm(n, false);
+        if constexpr (WG) wsync<WG>();  // the rank-1 update's stores before another lane's row reads
         for (int j = l; j < n; j += kWave) {  // one lane per row: the reference's serial sum
             T s = T(0);
-            for (int i = 0; i < n; ++i) s += Wl[j * ldl + i] * Wl[j * ldl + i];
+            for (int i = 0; i < n; ++i) {
+                const T x = wld<WG>(Wl + (int64_t)j * ldl + i);
+                s += x * x;
+            }
             const T len = sqrt(s);
-            for (int i = 0; i < n; ++i) Wl[j * ldl + i] = Wl[j * ldl + i] / len;
+            for (int i = 0; i < n; ++i) wst<WG>(Wl + (int64_t)j * ldl + i, wld<WG>(Wl + (int64_t)j * ldl + i) / len);
         }
-        __syncthreads();
+        wsync<WG>();
         // transRNorm on head, tail and entity[relation] (:185-187)
         OWNER_MARK(5);
-        transr_norm(E[0], Wl, ldl, abuf, n, lr OWNER_PC_ARG);
-        transr_norm(E[tslot], Wl, ldl, abuf, n, lr OWNER_PC_ARG);
-        transr_norm(E[eslot], Wl, ldl, abuf, n, lr OWNER_PC_ARG);
+        transr_norm<T, CH, WG>(E[0], Wl, ldl, abuf, n, lr OWNER_PC_ARG);
+        transr_norm<T, CH, WG>(E[tslot], Wl, ldl, abuf, n, lr OWNER_PC_ARG);
+        transr_norm<T, CH, WG>(E[eslot], Wl, ldl, abuf, n, lr OWNER_PC_ARG);
         R.store(a.rel + (int64_t)d.r * a.ld, n);
         for (int q = 0; q < d.count; ++q) row_store_sc1(E[q], a.ent + (int64_t)d.ent[q] * a.ld, n);
         drain_stores();
@@ -1135,9 +1161,9 @@ __global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32
         OWNER_MARK(8);
         OWNER_COUNT(11);
     }
-    __syncthreads();
+    wsync<WG>();
     if (cur >= 0) {
-        w_spill(Wl, ldl, a.w + (int64_t)cur * n * a.ld, n, a.ld);
+        if (!WG) w_spill(Wl, ldl, a.w + (int64_t)cur * n * a.ld, n, a.ld);
         if (l == 0) a.wtouched[cur] = stamp;
     }
 #ifdef KB2E_OWNER_PROF

@@ -707,8 +707,9 @@ static __attribute__((unused)) __global__ __launch_bounds__(kDaRelThreads) void 
     relation_records<kDaRelThreads>(a, bf, r, p0, ns, Wt, LT, gb, list, wsum);
 }
 
-// The pair records for n <= 128: transr_cons_da_kernel with two elements a lane
-// (G_i, i = 2l, 2l + 1; da_j = sum_i W[j][i] G_i by interleaved wave sums).
+// The pair records for n <= 128, a wave a record over the whole record array
+// (KB2E_RPAR_DA=wave; two elements a lane, G_i, i = 2l, 2l + 1; da_j = sum_i
+// W[j][i] G_i by interleaved wave sums, W from L2).
 static __attribute__((unused)) __global__ __launch_bounds__(256) void transr_cons_da_wide_kernel(RParArgs a,
                                                                                                  RParBufs<double> bf) {
     using T = double;

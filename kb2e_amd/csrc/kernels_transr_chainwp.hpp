@@ -192,67 +192,37 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
     bool changed = false;
     // the chunk whose W_c update and pair records the helpers still owe (nv 0: none)
     int pend_nv = 0, pend_par = 0, pend_pc = 0, pend_ka = 0, pend_base = 0;
-    if (tid == 0) {  // (misc[0] was read by every thread before the barriers above)
-        misc[5] = 0;   // helper-wave arrivals (helper_sync)
-        misc[6] = -1;  // the chunk whose walk is complete
-        misc[7] = -1;  // (chunk << 6) | violators published so far
-    }
     __syncthreads();
     tick(0);
 
-    // rows of chunk [b, e) of the list: R x NC elements, staged by waves 5-7 (RPT a
-    // thread, in registers) while waves 1-4 fold the walk's violators
-    constexpr int kRT = NT - 5 * 64, kRT0 = 5 * 64;  // the row-staging threads
-    constexpr int RPT = (R * NC + kRT - 1) / kRT;
-    static_assert(RPT <= 32, "rows_ok bits");
-    const bool rower = tid >= kRT0;
-    const int rt_ = tid - kRT0;
+    // rows of chunk [b, e) of the list: R x NC elements, RPT a thread, into registers
+    constexpr int RPT = (R * NC + NT - 1) / NT;
     T rows[RPT];
     uint32_t rows_ok = 0;
     auto load_rows = [&](int b, int e) {
-        if (!rower) return;
         int ent[RPT];
 #pragma unroll
         for (int q = 0; q < RPT; ++q) {
-            const int idx = rt_ + q * kRT;
+            const int idx = tid + q * NT;
             const int f = b + idx / NC;
             ent[q] = idx < R * NC && f < e ? pe[f] : -1;
         }
         rows_ok = 0;
 #pragma unroll
         for (int q = 0; q < RPT; ++q) {
-            const int j = (rt_ + q * kRT) % NC;
+            const int j = (tid + q * NT) % NC;
             const bool ok = ent[q] >= 0 && j < n;
             rows[q] = bf.ent[ok ? (uint32_t)ent[q] * (uint32_t)ld + (uint32_t)j : 0u];
             rows_ok |= (ok ? 1u : 0u) << q;
         }
     };
     auto store_rows = [&](int slot) {
-        if (!rower) return;
 #pragma unroll
         for (int q = 0; q < RPT; ++q) {
-            const int idx = rt_ + q * kRT;
+            const int idx = tid + q * NT;
             if (idx < R * NC) Abuf[slot * R * LA + (idx / NC) * LA + idx % NC] = ((rows_ok >> q) & 1) ? rows[q] : T(0);
         }
     };
-    // The helper waves meet without the walker (no s_barrier): every helper has paid
-    // its debt and written its tiles.  Bounded; a timeout sets *bf.err (the host
-    // fails loudly) and gives up.
-    int hsync_target = 0;
-    auto helper_sync = [&]() {
-        hsync_target += NW - 1;
-        if (l == 0) __hip_atomic_fetch_add(&misc[5], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        for (uint32_t sp = 0;
-             __hip_atomic_load(&misc[5], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < hsync_target; ++sp) {
-            if (sp > (1u << 22)) {
-                if (l == 0) __hip_atomic_store(bf.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    };
-    // KB2E_CONS_DBG bit 1: the old two-barrier chunk (all threads fold after the walk, A/B)
-    const bool fold_inc_on = !(bf.dbg & 2);
     // helpers: X = A W_c on their column tile (KS k-steps, B from the registers);
     // wave 4 also the chunk's Gram matrix A A^T (its B operand is its A operand),
     // wave 5 the cross Gram A A_c^T with the current chunk (Ac; none for a fresh chunk)
@@ -275,7 +245,7 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
 #pragma unroll
             for (int q = 0; q < 4; ++q) G[(kq + 4 * q) * LG + l16] = ga[q];
         }
-        if (w == 5 && Ac && !fold_inc_on) {  // the cross Gram with the current chunk's rows (the fold's dots)
+        if (w == 5 && Ac) {  // the cross Gram with the current chunk's rows (the fold's dots)
             typename M::acc_t ca = {T(0), T(0), T(0), T(0)};
 #pragma unroll
             for (int q = 0; q < KS; ++q) ca = M::mma(av[q], Ac[l16 * LA + 4 * q + kq], ca);
@@ -339,64 +309,6 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
         sq += __shfl_xor(sq, 16);
         if ((tid & 31) == 0 && j < R) qpart[j] = j < cn ? sq : T(0);
     };
-    // The fold of chunk k's violators into X_{k+1} by waves 1-4 while the walker walks
-    // (kernels_transr_pipe.hpp correct_inc): each violator v as soon as it is
-    // published (misc[7] = (chunk << 6) | count, after its G row and vl entry;
-    // misc[6] = chunk when the walk ends), its dots a_{k+1}[j] . a_v on the fly (the
-    // fold needs them for the chunk's few violators only: no cross Gram on the matrix
-    // cores), so after the walk only its last violators remain; then |p_j|^2.
-    // Sixteen threads a row (one DPP row), columns c = (t & 15) + 16 u.
-    auto fold_inc = [&](T* Pn, int cn, const T* Pc, const T* An, const T* Ac, const int* vl, int ck) {
-        constexpr int NU = (NC + 15) / 16;
-        const int t4 = tid - 64, j = t4 >> 4, c0 = t4 & 15;
-        const bool okr = j < cn;
-        T x[NU], an[NU];
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            const int c = c0 + 16 * u;
-            x[u] = okr && c < NC ? Pn[j * LA + c] : T(0);
-            an[u] = okr && c < NC ? An[j * LA + c] : T(0);
-        }
-        int used = 0;
-        for (uint32_t sp = 0;; ++sp) {
-            const bool done = __hip_atomic_load(&misc[6], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == ck;
-            const int pw = __hip_atomic_load(&misc[7], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int avail = (pw >> 6) == ck ? (pw & 63) : 0;
-            for (; used < avail; ++used) {
-                const int v = vl[used];
-                T d[1] = {T(0)};
-#pragma unroll
-                for (int u = 0; u < NU; ++u) {
-                    const int c = c0 + 16 * u;
-                    if (c < NC) d[0] = fma(an[u], Ac[v * LA + c], d[0]);
-                }
-                row16_sums<T, 1>(d);
-                const T gl = -lr * d[0];
-#pragma unroll
-                for (int u = 0; u < NU; ++u) {
-                    const int c = c0 + 16 * u;
-                    if (c < NC) x[u] = fma(gl, Pc[v * LA + c], x[u]);
-                }
-            }
-            if (done) break;
-            if (sp > (1u << 22)) {
-                if (l == 0) __hip_atomic_store(bf.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        T sq[1] = {T(0)};
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            const int c = c0 + 16 * u;
-            if (okr && c < NC) {
-                if (used) Pn[j * LA + c] = x[u];
-                sq[0] = fma(x[u], x[u], sq[0]);
-            }
-        }
-        row16_sums<T, 1>(sq);
-        if (c0 == 0) qpart[j] = okr ? sq[0] : T(0);
-    };
     // W_c's unit rows (transr/trainer.cpp:178-180) before the last update's pairs;
     // row sums of the tiles in DPP rows, then LDS (the P buffers are free: drained)
     auto renorm = [&] {
@@ -423,11 +335,10 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
     };
     // the walk of one chunk (wave 0): pairs [base, base + cc), projections in P (rows
     // j < cc), |p_j|^2 in qpart, rows in A; the violators' rows of P become G
-    auto walk = [&](T* P, const T* Gm, int cc, int base, int* vl, int ck, int par) {
+    auto walk = [&](T* P, const T* Gm, int cc, int base, int* vl) {
         const int j = l & (R - 1), h = l >> 4;  // lane: quarter h of row j
         T q = j < cc ? qpart[j] : T(0);
         uint32_t vmask = 0;
-        int npub = 0;  // violators published to the folding waves (fold_inc)
         if (__ballot(j < cc && q > T(1)) != 0) {
             T x[KS];
 #pragma unroll
@@ -444,12 +355,8 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
 #pragma unroll
                     for (int u = 0; u < KS; ++u) P[v * LA + h * KS + u] = x[u];
                 }
-                // a_j . a_v for every row, from the chunk's Gram matrix; the scalars known
-                // at the pick, ahead of V: |p_v|^2, its reciprocal, |a_v|^2
+                // a_j . a_v for every row, from the chunk's Gram matrix
                 const T dp = Gm[j * LG + v];
-                const T pp = readlane_f(q, v);
-                const T rpp = T(1) / pp;
-                const T aa = readlane_f(dp, v);
                 // V_c = sum_i p_v[i] K0[i][c], c = l and l + 64: 16-byte reads of K0's row
                 // pairs (consecutive lanes, consecutive pairs), p_v as broadcasts; the
                 // second column's reads are clamped, not branched (its lanes >= NC - 64
@@ -495,9 +402,11 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
                 const T pv0 = pr[l], pv1 = c1 < NC ? pr[c1] : T(0);
                 T s2[2] = {pv0 * V0 + pv1 * V1, V0 * V0 + V1 * V1};
                 wave_sums<T, 2>(s2);
+                const T pp = readlane_f(q, v);
+                const T aa = readlane_f(dp, v);  // |a_v|^2
                 const T pV = s2[0], VV = s2[1];
                 const T pvd = pV + aa * pp, vvd = VV + T(2) * aa * pV + aa * aa * pp;
-                const T kappa = pvd * rpp;
+                const T kappa = pvd / pp;
                 const T w2t = vvd - kappa * pvd;
                 const T w2 = w2t > T(0) ? w2t : T(0);
                 const T rho = T(1) - eps * kappa;
@@ -526,24 +435,19 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
                 qh += __shfl_xor(qh, 16);
                 qh += __shfl_xor(qh, 32);
                 if (upd) q = qh;
-                // publish v to the folding waves: its G row (above) and vl entry first
-                if (l == 0) {
-                    vl[npub] = v;
-                    __hip_atomic_store(&misc[7], (ck << 6) | (npub + 1), __ATOMIC_RELEASE,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-                ++npub;
                 vmask |= 1u << v;
                 cursor = v + 1;
                 ++n_vio;
                 tick(15);
             }
         }
-        if (l < R && ((vmask >> l) & 1u)) vflag[base + l] = 1;
+        if (l < R && ((vmask >> l) & 1u)) {
+            vl[__builtin_popcount(vmask & ((1u << l) - 1u))] = l;
+            vflag[base + l] = 1;
+        }
         if (l == 0) {
-            misc[1 + 2 * par] = (int)vmask;
-            misc[2 + 2 * par] = npub;
-            __hip_atomic_store(&misc[6], ck, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            misc[1] = (int)vmask;
+            misc[2] = __builtin_popcount(vmask);
         }
     };
     // the pipeline over the list's pairs [0, npw) (pe / ps), chunks of R; ends
@@ -573,49 +477,38 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
             const T* Gm = Gbuf + pc * R * LG;
             T* Gn = Gbuf + (pc ^ 1) * R * LG;
             int* vl = vlist + pc * R;
-            const int ck = (int)n_chunks;  // the chunk's tag in the publish words (misc[6], misc[7])
             ++n_chunks;
             if (w == 0) {
-                walk(P, Gm, cc, k * R, vl, ck, pc);
+                walk(P, Gm, cc, k * R, vl);
                 tick(2);
             } else {
                 apply_pending();  // chunk k - 1's
                 tick(10);
                 if (cn > 0 && !(bf.dbg & 1)) x_tile(An, Pn, Gn, A);
                 tick(11);
-                if (fold_inc_on) {
-                    // every helper past its debt (chunk k-1's A slot free) and its tile (X_{k+1} whole)
-                    helper_sync();
-                    if (k + 2 < nch) {  // chunk k + 2's rows into the slot chunk k - 1 left, k + 3's in flight
-                        store_rows((k + 2) % 3);
-                        if (k + 3 < nch) load_rows((k + 3) * R, (k + 3) * R + csz(k + 3));
-                    }
-                    if (cn > 0 && w <= 4) fold_inc(Pn, cn, P, An, A, vl, ck);
-                }
             }
-            __syncthreads();  // B1: the walk's G rows and violators, P_{k+1} and its |p|^2
+            __syncthreads();  // B1: the walk's G rows and violators, X_{k+1}
             tick(w == 0 ? 3 : 12);
             if (bf.dbg & 1) {  // (timing experiment: the projections after the walk, not beside it)
                 if (w > 0 && cn > 0) x_tile(An, Pn, Gn, A);
                 __syncthreads();
             }
-            const int nv = misc[2 + 2 * pc];
+            const int nv = misc[2];
             pend_nv = nv;
             pend_par = pc;
             pend_pc = pc;
             pend_ka = ka;
             pend_base = k * R;
             if (nv) changed = true;
-            if (!fold_inc_on) {  // (A/B: the two-barrier chunk)
-                if (k + 2 < nch) {
-                    store_rows((k + 2) % 3);
-                    if (k + 3 < nch) load_rows((k + 3) * R, (k + 3) * R + csz(k + 3));
-                }
-                if (cn > 0) fold(Pn, cn, nv, P, vl);
-                tick(4);
-                __syncthreads();  // B2: P_{k+1} and its |p|^2
-                tick(5);
+            // chunk k + 2's rows into the slot chunk k - 1 left, chunk k + 3's in flight
+            if (k + 2 < nch) {
+                store_rows((k + 2) % 3);
+                if (k + 3 < nch) load_rows((k + 3) * R, (k + 3) * R + csz(k + 3));
             }
+            if (cn > 0) fold(Pn, cn, nv, P, vl);
+            tick(4);
+            __syncthreads();  // B2: P_{k+1} and its |p|^2
+            tick(5);
         }
         apply_pending();
         pend_nv = 0;

@@ -51,7 +51,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
     static_assert(sizeof(T) == 8, "the D-row / k-step identity below is the FP64 fragment layout");
     constexpr int NB = (4 * KS + 15) / 16;  // column slices of 16
     constexpr int NP = 16 * NB, L = NP + 2, R = kChainRows, LG = R + 1;
-    constexpr int NH = NP / 2;              // columns of a row half (walk registers)
+    constexpr int NH = 2 * KS;              // columns of a row half (walk registers; 4 KS >= n, the rest zero)
     constexpr int NSW = (NB + 2) / 3;       // column slices a helper wave owns (slice cb: wave 1 + cb % 3)
     static_assert(2 * R * L >= NP * L, "the K0 image borrows the two P buffers");
     static_assert(NSW * KS <= 4 * KS, "the helpers' slices share the walk's K0 registers");
@@ -82,8 +82,10 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
     __shared__ unsigned long long ph[16];  // (LDS, not sixteen 64-bit registers)
     if (threadIdx.x < 16) ph[threadIdx.x] = 0;
     long long tq = ck0;
+    // (phases 12..15 on thread 64, helper wave 1: debt, tiles, helper_sync wait, rows +
+    // corrections incl. the wait for the walk's end)
     auto tick = [&](int k) {
-        if (bf.stats && threadIdx.x == 0) {
+        if (bf.stats && threadIdx.x == (k >= 12 || k == 5 ? 64u : 0u)) {
             const long long t = clock64();
             ph[k] += (unsigned long long)(t - tq);
             tq = t;
@@ -269,7 +271,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
     // |p_j|^2 partials (qpart[0], the other slices' partials zero).  Sixteen threads a
     // row (one DPP row), NP / 16 columns each, rows rs, rs + 12, rs + 24.  The same
     // FMAs per element in the same order as correct_q.
-    auto correct_inc = [&](T* Pn, int cn, const T* Pc, const int* vl, int ck) {
+    auto correct_inc = [&](T* Pn, int cn, const T* Pc, const T* An, const T* Ac, const int* vl, int ck) {
         constexpr int NE = NP / 16, NPS = (R + 11) / 12;
         const int rs = ht >> 4, cb = (ht & 15) * NE;
         T x[NPS][NE];
@@ -286,14 +288,25 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
             const int avail = (pw >> 6) == ck ? (pw & 63) : 0;
             for (; used < avail; ++used) {
                 const int v = vl[used];
-                T gv[NE];
+                T gv[NE], av[NE], d[NPS];
 #pragma unroll
-                for (int u = 0; u < NE; ++u) gv[u] = Pc[v * L + cb + u];
+                for (int u = 0; u < NE; ++u) {
+                    gv[u] = Pc[v * L + cb + u];
+                    av[u] = Ac[v * L + cb + u];
+                }
+#pragma unroll
+                for (int p = 0; p < NPS; ++p) {  // a_{k+1}[j] . a_v, this thread's columns
+                    const int j = rs + 12 * p;
+                    d[p] = T(0);
+#pragma unroll
+                    for (int u = 0; u < NE; ++u) d[p] = fma(j < R ? An[j * L + cb + u] : T(0), av[u], d[p]);
+                }
+                row16_sums<T, NPS>(d);
 #pragma unroll
                 for (int p = 0; p < NPS; ++p) {
                     const int j = rs + 12 * p;
                     if (j < cn) {
-                        const T gl = -lr * Cx[j * LG + v];
+                        const T gl = -lr * d[p];
 #pragma unroll
                         for (int u = 0; u < NE; ++u) x[p][u] = fma(gl, gv[u], x[p][u]);
                     }
@@ -561,8 +574,8 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                         const int c = l;  // column
                         // the scalars known at the pick, ahead of V: |p_v|^2, 1 / |p_v|^2, |a_v|^2
                         const T pp = readlane_f(q, v);
-                        const T rpp = T(1) / pp;
                         const T aa = readlane_f(aaj, v);
+                        const T cjv = Gm[j * LG + v];  // a_j . a_v for the later rows' update
                         // the violator's current row to LDS for the column-lane layout
                         if (j == v) {
 #pragma unroll
@@ -578,6 +591,10 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                         const T Vc = c < n ? (vv4[0] + vv4[1]) + (vv4[2] + vv4[3]) : T(0);
                         tick(7);
                         T s2[2] = {pv * Vc, Vc * Vc};
+                        // 1 / |p_v|^2: v_rcp_f64 and one Newton step (three dependent ops, not
+                        // the IEEE division's ten; kappa moves by an ulp or so)
+                        T rpp = __builtin_amdgcn_rcp(pp);
+                        rpp = fma(fma(-pp, rpp, T(1)), rpp, rpp);
                         wave_sums<T, 2>(s2);
                         tick(8);
                         const T pV = s2[0], VV = s2[1];
@@ -598,7 +615,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                         const bool upd = j > v && j < cc;
                         T qh = T(0);  // this lane's half of |p_j|^2
                         if (upd) {
-                            const T gl = -lr * Gm[j * LG + v];
+                            const T gl = -lr * cjv;
                             T s4[4] = {T(0), T(0), T(0), T(0)};
 #pragma unroll
                             for (int u = 0; u < NH; ++u) {
@@ -641,21 +658,34 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                 // X = A_{k+1} W_c (each helper its own slices), its Gram matrix and the cross
                 // Gram A_{k+1} A_k^T (waves 2 and 3)
                 apply_pending();
+                tick(12);
                 if (cn > 0) {
                     const int nrt = cn > 16 ? 2 : 1, crt = cc > 16 ? 2 : 1;
 #pragma unroll
                     for (int si = 0; si < NSW; ++si)
                         if (hw + 3 * si < NB)
                             for (int rt = 0; rt < nrt; ++rt) proj_tile(An, rt, si, Pn);
+                    // the Gram tiles to the helpers with the fewest projection tiles (the
+                    // same greedy choice on every helper); no cross Gram: correct_inc takes
+                    // the few violators' dots a_{k+1}[j] . a_v on the fly
                     const int ng = nrt == 2 ? 3 : 1;
-                    for (int tl = hw; tl < ng + nrt * crt; tl += 3) {
-                        if (tl < ng) gram_tile(An, An, tl == 0 ? 0 : 1, tl == 2 ? 1 : 0, Gn, LG);
-                        else gram_tile(An, A, (tl - ng) / crt, (tl - ng) % crt, Cx, LG);
+                    int load[3];
+#pragma unroll
+                    for (int h = 0; h < 3; ++h) load[h] = nrt * ((NB - h + 2) / 3);  // slices h, h + 3, ...
+                    for (int tl = 0; tl < ng; ++tl) {
+                        int best = 0;
+#pragma unroll
+                        for (int h = 1; h < 3; ++h) best = load[h] < load[best] ? h : best;
+                        ++load[best];
+                        if (best == hw) gram_tile(An, An, tl == 0 ? 0 : 1, tl == 2 ? 1 : 0, Gn, LG);
                     }
+                    (void)crt;
                 }
                 // every helper past its debt (chunk k-1's A slot and G rows are free) and its
                 // tiles (P_n, the Gram matrices complete)
+                tick(13);
                 helper_sync();
+                tick(14);
                 // chunk k+2's rows into the slot chunk k-1 left, chunk k+3's in flight
                 if (nb2 < npairs || cn > 0) {
                     store_rows(ka == 0 ? 2 : ka - 1);
@@ -663,10 +693,11 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                     load_rows(n3, n3 < npairs ? chunk_end(n3) : n3);
                 }
                 // chunk k's violators into P_{k+1} as the walker publishes them, then |p|^2
-                if (cn > 0) correct_inc(Pn, cn, P, vl, ck);
+                if (cn > 0) correct_inc(Pn, cn, P, An, A, vl, ck);
+                tick(15);
             }
             __syncthreads();  // B1: the walk, the next chunk's corrected projections and |p|^2
-            tick(3);
+            tick(w == 0 ? 3 : 5);
             const uint32_t vmask = (uint32_t)misc[1 + 2 * par];
             const int nv = misc[2 + 2 * par];
             // chunk k's debt passes to the helpers (paid at the next chunk, or below)

@@ -38,9 +38,8 @@
 // the chunk as P_j -= lr (a_j . a_v) g (the Gram entry), |p_j|^2 made afresh --
 // no barrier between violators.  The chunk's violators then update W_c (the G
 // rows kept in P), before the next chunk's P.  ~1.7 of 16 pairs violate on
-// FB15k-shaped data.  The pair records da = -lr W G are made afterwards, one
-// wave a violator, over the final matrix (transr_cons_da_kernel: first order
-// the same, off the chain).
+// FB15k-shaped data.  The pair records da = -lr W G are made at the end of the
+// relation's chain over its final matrix (chain_records: first order the same).
 #pragma once
 
 #include "kernels_transr_mfma.hpp"
@@ -146,10 +145,11 @@ template <typename T>
 __device__ __forceinline__ int transr_rounds_violator4(T Q0, T w2, T eps, T rho, T& S0, T& S1) {
     const T e2w = eps * eps * w2;
     const T r1 = rho, r2 = r1 * rho, r3 = r2 * rho, r4 = r3 * rho;
+    // (bitwise &: no short-circuit branches between the tests)
     const bool c1 = r1 * r1 * Q0 + e2w * T(1) * T(1) * T(1) * T(1) > T(1);
-    const bool c2 = c1 && r2 * r2 * Q0 + e2w * T(2) * T(2) * r1 * r1 > T(1);
-    const bool c3 = c2 && r3 * r3 * Q0 + e2w * T(3) * T(3) * r2 * r2 > T(1);
-    const bool c4 = c3 && r4 * r4 * Q0 + e2w * T(4) * T(4) * r3 * r3 > T(1);
+    const bool c2 = c1 & (r2 * r2 * Q0 + e2w * T(2) * T(2) * r1 * r1 > T(1));
+    const bool c3 = c2 & (r3 * r3 * Q0 + e2w * T(3) * T(3) * r2 * r2 > T(1));
+    const bool c4 = c3 & (r4 * r4 * Q0 + e2w * T(4) * T(4) * r3 * r3 > T(1));
     S0 = T(1);
     S1 = T(0);
     S0 += c1 ? r1 : T(0);
@@ -698,56 +698,6 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_chain_kernel(RParAr
                 atomicAdd(&g_seq_stats[42], n_vio);
             }
         }
-    }
-}
-
-// The pair records of the batch's violators: G (left there by the chain kernel)
-// -> da = -lr W G with the relation's final matrix (transr/trainer.cpp:59-60,
-// first order in lr the same as the matrix at the pair's chunk).  The records
-// are the update slots of active samples with pflag set (4 B of them) and the
-// relations whose (entity[r], r) record carries this batch's stamp.  One wave a
-// record: lane i holds G_i, da_j = sum_i W[j][i] G_i by wave reductions.
-template <typename T>
-__global__ __launch_bounds__(256) void transr_cons_da_kernel(RParArgs a, RParBufs<T> bf) {
-    const int n = a.n, ld = a.ld, l = lane_id();
-    const int nrec = 4 * a.B + a.nr;
-    // one wave a record (grid: every record), so a record's dependent loads are
-    // the kernel's whole latency
-    {
-        const int q = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-        if (q >= nrec) return;
-        // the validity flags, the sample id and the G row are independent loads:
-        // issued together, then the relation, then its matrix rows
-        int r;
-        T* row;
-        bool ok;
-        if (q < 4 * a.B) {
-            const uint8_t ac = a.act[q >> 2], pf = bf.pflag[q];
-            const int i0 = a.si[q >> 2];
-            row = bf.pair + (int64_t)q * ld;
-            ok = ac && pf;
-            r = ok ? a.rels[i0] : 0;
-        } else {
-            r = q - 4 * a.B;
-            row = bf.relpair + (int64_t)r * ld;
-            ok = bf.relpair_stamp[r] == bf.stamp;
-        }
-        const T gi = l < n ? row[l] : T(0);  // (a row of the buffer even when unused)
-        if (!ok) return;
-        const T* W = bf.W + (int64_t)r * n * ld;
-        T da = T(0);
-        // eight rows of W at a time: their loads in flight together and eight
-        // interleaved wave reductions instead of one dependent chain a row
-        for (int j0 = 0; j0 < n; j0 += 8) {
-            T v[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = (l < n && j0 + k < n) ? W[(int64_t)(j0 + k) * ld + l] * gi : T(0);
-            wave_sums<T, 8>(v);
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (l == j0 + k) da = v[k];
-        }
-        if (l < n) row[l] = -(T)a.lr * da;
     }
 }
 

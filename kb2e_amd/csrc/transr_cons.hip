@@ -14,6 +14,7 @@
 #include "kernels_transr_seq.hpp"
 #include "kernels_transr_chainw.hpp"
 #include "kernels_transr_chainwp.hpp"
+#include "kernels_transr_chaing.hpp"
 #include "kernels_transr_pipe.hpp"
 #include "kernels_transr_wave.hpp"
 
@@ -116,13 +117,12 @@ size_t cons_seq_setup(int n) {
     return lds;
 }
 
-void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, int grid, size_t lds, hipStream_t stream) {
+void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, size_t lds, hipStream_t stream) {
     RParArgs aa = a;
     RParBufs<double> bb = bf;
     void* args[] = {&aa, &bb};
     // (the LDS size was chosen by cons_seq_setup under the same switch)
     // one workgroup per relation, most frequent first (chain_first_tile; those absent exit)
-    (void)grid;
     // (the pair records are made at the end of each relation's chain: chain_records)
     HIPCHK(hipLaunchKernel(lds == pipe_lds<double>(a.n) && use_pipe() ? pipe_fn(a.n) : chain_fn(a.n), dim3(a.nr),
                            dim3(kChainThreads), args, lds, stream));
@@ -198,6 +198,28 @@ void proj_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, hipStr
     const size_t lds = sizeof(T) * (size_t)proj_wave_rows<T>(cons_live_steps<T>(a.n)) * rm_ld(a.n);
     HIPCHK(hipLaunchKernel(kernel_fn<T>(kProj, a.n), dim3(grid), dim3(kProjWaves * kWave), args, lds, stream));
 }
+
+bool cons_chaing_supported(int n) { return n >= 1 && n <= kGenMaxN; }
+
+size_t cons_chaing_setup(int n, int esize) {
+    const size_t lds = chaing_lds(n);
+    HIPCHK(hipFuncSetAttribute(esize == 8 ? (const void*)transr_cons_chain_gen_kernel<double>
+                                          : (const void*)transr_cons_chain_gen_kernel<float>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    return lds;
+}
+
+template <typename T>
+void cons_chaing_launch(const RParArgs& a, const RParBufs<T>& bf, size_t lds, hipStream_t stream) {
+    RParArgs aa = a;
+    RParBufs<T> bb = bf;
+    void* args[] = {&aa, &bb};
+    // one workgroup per relation, most frequent first (those absent from the batch exit)
+    HIPCHK(hipLaunchKernel((const void*)transr_cons_chain_gen_kernel<T>, dim3(a.nr), dim3(kGenThreads), args, lds,
+                           stream));
+}
+template void cons_chaing_launch<double>(const RParArgs&, const RParBufs<double>&, size_t, hipStream_t);
+template void cons_chaing_launch<float>(const RParArgs&, const RParBufs<float>&, size_t, hipStream_t);
 
 template void proj_wave_launch<double>(const RParArgs&, const RParBufs<double>&, int, hipStream_t);
 template void proj_wave_launch<float>(const RParArgs&, const RParBufs<float>&, int, hipStream_t);

@@ -27,12 +27,13 @@ void proj_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, hipStr
 // (kernels_transr_wave.hpp); needs bf.x, bf.d and the hinge decisions in place.
 template <typename T>
 void grad_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, hipStream_t stream);
-// transRNorm per relation as a chain of 16-pair chunks (kernels_transr_seq.hpp; FP64,
-// n <= 64): dynamic LDS bytes (and the kernel's limit raised to it); launch of the chain
-// (one workgroup per tile of the batch; a relation's first tile does the work) and of
-// the pair records' kernel after it.
+// transRNorm per relation, pair by pair, in chunks of 32 (kernels_transr_pipe.hpp, or
+// the unpipelined kernels_transr_seq.hpp under KB2E_RPAR_CHAIN=serial; FP64, n <= 64):
+// dynamic LDS bytes (and the kernel's limit raised to it); the launch, one workgroup per
+// relation, most frequent first (those absent from the batch exit), each making its
+// relation's pair records at the end of its chain (chain_records).
 size_t cons_seq_setup(int n);
-void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, int grid, size_t lds, hipStream_t stream);
+void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, size_t lds, hipStream_t stream);
 // transRNorm per relation, pair by pair, for n <= 112 (kernels_transr_chainw.hpp,
 // kernels_transr_chainwp.hpp; FP64,
 // any path: the VALU tile kernels at n = 100): is the width covered, its dynamic LDS
@@ -41,6 +42,14 @@ void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, int grid, si
 bool cons_chainw_supported(int n);
 size_t cons_chainw_setup(int n);
 void cons_chainw_launch(const RParArgs& a, const RParBufs<double>& bf, size_t lds, hipStream_t stream);
+// transRNorm per relation, pair by pair, for FP32 tables and 112 < n <= 128
+// (kernels_transr_chaing.hpp; the same model, double arithmetic, no matrix cores):
+// is the width covered, its dynamic LDS (the limit raised to it), and the launch (one
+// workgroup per relation, most frequent first; its pair records made in-kernel).
+bool cons_chaing_supported(int n);
+size_t cons_chaing_setup(int n, int esize);
+template <typename T>
+void cons_chaing_launch(const RParArgs& a, const RParBufs<T>& bf, size_t lds, hipStream_t stream);
 // Does that chain run software-pipelined at this width (64 < n <= 100,
 // kernels_transr_chainwp.hpp; KB2E_RPAR_CHAIN=lockstep: the eight-wave lockstep kernel)?
 bool cons_chainw_pipelined(int n);

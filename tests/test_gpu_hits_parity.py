@@ -24,11 +24,15 @@ its ORDERED run ends *below* the seed tables' Hits@10 (1.1 % after 150 epochs
 against 2.5 % for the seed alone on this set), so only the schedule delta is
 asserted for it.
 
-TransR runs at the north-star width n = 50, and the loss trajectory is bounded
-too: the mean loss of the last 10 epochs within LOSS_TOL_REL of ORDERED's.  On
-the FB15k-shaped set the ORDERED seed envelope (5 glibc seeds) spans +-3.6 %
-around its mean and PARALLEL sits 2.6 % below it
-(profiles/seed_envelope_r17_fb15k_R_compat.jsonl, .._r18_.._parallel_seq.jsonl).
+TransR runs at the north-star width n = 50 and at K5's n = 100 (fixed energy,
+the form that learns), and the loss trajectory is bounded too: the mean loss of
+the last 10 epochs within LOSS_TOL_REL of ORDERED's.  On the FB15k-shaped set
+the ORDERED seed envelope (5 glibc seeds) spans +-3.6 % around its mean and
+PARALLEL compat sits 2.6 % below it at n = 50
+(profiles/seed_envelope_r17_fb15k_R_compat.jsonl, .._r18_.._parallel_seq.jsonl);
+with fixed energy at n = 100 the paired gap is +0.16 % [-0.04, +0.36]
+(profiles/seed_envelope_r22_fb15k_R100_fixed.jsonl), so fixed energy is held
+to LOSS_TOL_FIXED.
 """
 import pytest
 
@@ -40,6 +44,7 @@ pytestmark = pytest.mark.gpu
 HITS_TOL_PP = 0.5
 RANK_TOL_REL = 0.02
 LOSS_TOL_REL = 0.05
+LOSS_TOL_FIXED = 0.02
 
 
 @pytest.fixture(scope="module")
@@ -52,6 +57,7 @@ def ds():
     ("H", 50, 300, True, True),
     ("R", 50, 50, False, True),   # fixed energy
     ("R", 50, 50, True, False),   # compat energy (the reference default)
+    ("R", 100, 50, False, True),  # K5's width: the pipelined wide chain (kernels_transr_chainwp.hpp), fixed energy
 ])
 def test_parallel_schedule_matches_reference_hits10(ds, model, dim, epochs, compat, learns):
     out = schedule_parity(ds, model, dim, epochs, seed_epochs=300, rate=0.001, method=1, batches=100, seed=7,
@@ -68,4 +74,5 @@ def test_parallel_schedule_matches_reference_hits10(ds, model, dim, epochs, comp
     # and the loss trajectory: the last 10 epochs' mean loss
     lo = sum(x[1] for x in o["losses"][-10:]) / 10
     lp = sum(x[1] for x in p["losses"][-10:]) / 10
-    assert abs(lp - lo) <= LOSS_TOL_REL * lo, (lp, lo)
+    print("last-10 loss", lp, lo, (lp - lo) / lo)
+    assert abs(lp - lo) <= (LOSS_TOL_REL if compat or model != "R" else LOSS_TOL_FIXED) * lo, (lp, lo)

@@ -92,7 +92,7 @@ def _cons_form(dim, mfma):
     ck = os.environ.get("KB2E_RPAR_CONS", "")
     if ck in ("tile", "jacobi"):
         return "jacobi"
-    assert dim <= 112, "PARALLEL TransR above n = 112 runs only on request (KB2E_RPAR_CONS=jacobi)"
+    assert dim <= 128, "PARALLEL TransR trains n <= 128"
     return "chunk1"
 
 
@@ -101,8 +101,6 @@ def _transr_vs_model(ds, dim, epochs, monkeypatch, *, St=8, compat=False, distan
     from oracle.parallel import transr_parallel_batches
     monkeypatch.setenv("KB2E_RPAR_ST", str(St))
     monkeypatch.setenv("KB2E_RPAR_MFMA", "1" if mfma else "0")
-    if dim > 112:  # the Jacobi transRNorm is the only form there, and only on request
-        monkeypatch.setenv("KB2E_RPAR_CONS", "jacobi")
     cons = _cons_form(dim, mfma)
     m = orc.Model("R", dim, ds.num_entities, ds.num_relations, rate=rate, distance=distance, batches=batches,
                   transr_compat=compat)
@@ -224,6 +222,35 @@ def test_transr_parallel_compat_chunk_prefix(dim, mfma, monkeypatch):
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=2 if dim > 64 else 8, compat=True, mfma=mfma)
 
 
+def test_transr_parallel_compat_prefix_paths_agree(monkeypatch):
+    """Batches of more than kScanDirectMax chunks of the compat work-vector scan
+    (K5) take the chunk prefix from rpar_scan_prefix_kernel, which sums in another
+    order than every chunk block summing its own prefix.  On batches that large
+    (the small set in 2 batches: ~470 chunks each) both paths must give the same
+    hinge decisions up to margin ties and the same loss to rounding."""
+    ds = data.synthetic("small", seed=1)
+    out = {}
+    for pre in ("0", "1"):
+        monkeypatch.setenv("KB2E_RPAR_SCAN_PREFIX", pre)
+        eng = Engine("R", 50, ds.num_entities, ds.num_relations, rate=0.001, batches=2, seed=3, schedule="parallel")
+        eng.upload_triples(ds.train)
+        e0, r0, _ = eng.init_params()
+        eng.transr_seed(e0, r0)
+        out[pre] = [eng.train_epoch() for _ in range(2)]
+        eng.close()
+    for (l0, a0), (l1, a1) in zip(out["0"], out["1"]):
+        assert abs(a0 - a1) <= 2, (a0, a1)
+        assert abs(l0 - l1) <= 1e-9 * l0 + 2.0 * abs(a0 - a1), (l0, l1)
+
+
+@pytest.mark.parametrize("dim", [100, 128])
+def test_transr_parallel_rows8(dim, monkeypatch):
+    """KB2E_RPAR_ROWS8=1: the relation-row passes four rows a wave, eight elements a
+    lane (n <= 128; a different norm reduction order): the same model."""
+    monkeypatch.setenv("KB2E_RPAR_ROWS8", "1")
+    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=2, mfma=False)
+
+
 def _hub_dataset(ne=300, nr=6, count=4000, seed=5):
     """Entity 0 heads ~half the triples: its event segments run to hundreds of
     events a batch (pair_prev_long_kernel's LDS table path)."""
@@ -263,18 +290,59 @@ def test_transr_parallel_independent_of_tile_size(monkeypatch):
             assert max_abs(x, y) < 1e-12
 
 
-@pytest.mark.parametrize("dim,precision", [(120, 64), (50, 32)])
-def test_transr_parallel_refuses_without_chain(dim, precision, monkeypatch):
-    """PARALLEL TransR runs the pair-by-pair transRNorm (FP64, n <= 112); elsewhere
-    the context is refused (KB2E_EUNSUPPORTED) instead of silently taking the Jacobi
-    form, whose loss departs from the reference's -- unless asked for by name."""
+@pytest.mark.parametrize("dim,St,compat", [(120, 2, False), (128, 1, True), (113, 2, False)])
+def test_transr_parallel_generic_chain_wide(dim, St, compat, monkeypatch):
+    """112 < n <= 128: the pair-by-pair chain in double arithmetic without the matrix
+    cores (kernels_transr_chaing.hpp), the same CPU model as every other width."""
+    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=compat)
+
+
+@pytest.mark.parametrize("dim,St,compat,mfma", [(20, 8, False, True), (50, 8, True, True), (33, 4, True, False),
+                                                (100, 8, False, False)])
+def test_transr_parallel_generic_chain_forced(dim, St, compat, mfma, monkeypatch):
+    """KB2E_RPAR_CHAIN=gen: the generic chain where the matrix-core chains would run
+    (their model, so the same bar), on both phase-A paths."""
+    monkeypatch.setenv("KB2E_RPAR_CHAIN", "gen")
+    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=compat, mfma=mfma)
+
+
+def test_transr_parallel_generic_chain_windows(monkeypatch):
+    """The generic chain over several 128-sample windows of a relation (the small
+    set's hottest relation holds ~700 samples a batch): W_c and the held-back tail
+    carry across windows."""
+    monkeypatch.setenv("KB2E_RPAR_CHAIN", "gen")
+    _transr_vs_model(data.synthetic("small", seed=1), 50, 1, monkeypatch, St=8, compat=True, rate=0.001)
+
+
+def test_transr_parallel_refuses_above_128(monkeypatch):
+    """PARALLEL TransR trains n <= 128 (the VALU tile path holds two elements a
+    lane); wider contexts are refused (KB2E_EUNSUPPORTED: the ORDERED schedule
+    trains up to 138)."""
     from kb2e_amd.engine import EngineError
-    monkeypatch.delenv("KB2E_RPAR_CONS", raising=False)
     ds = tiny()
     with pytest.raises(EngineError, match="EUNSUPPORTED"):
-        Engine("R", dim, ds.num_entities, ds.num_relations, precision=precision, schedule="parallel")
-    monkeypatch.setenv("KB2E_RPAR_CONS", "jacobi")
-    Engine("R", dim, ds.num_entities, ds.num_relations, precision=precision, schedule="parallel").close()
+        Engine("R", 136, ds.num_entities, ds.num_relations, schedule="parallel")
+
+
+def test_transr_parallel_fp32_chain_close(monkeypatch):
+    """FP32 tables take the same pair-by-pair chain (double arithmetic, FP32
+    storage): epoch loss and active counts within 1 % of the FP64 run, the tables
+    within FP32 rounding drift (median 1e-3)."""
+    ds = data.synthetic("small", seed=1)
+    out, tabs = {}, {}
+    for prec in (64, 32):
+        eng = Engine("R", 50, ds.num_entities, ds.num_relations, rate=0.001, batches=10, seed=3, precision=prec,
+                     schedule="parallel", transr_compat=False)
+        eng.upload_triples(ds.train)
+        e0, r0, _ = eng.init_params()
+        eng.transr_seed(e0, r0)
+        out[prec] = [eng.train_epoch() for _ in range(2)]
+        tabs[prec] = eng.download_params()
+        eng.close()
+    for (l64, a64), (l32, a32) in zip(out[64], out[32]):
+        assert abs(a64 - a32) <= 0.01 * a64 and abs(l64 - l32) <= 0.01 * l64
+    for x, y in zip(tabs[64], tabs[32]):
+        assert np.median(np.abs(x - y)) < 1e-3
 
 
 def test_transr_parallel_fp32_close(monkeypatch):

@@ -47,10 +47,13 @@ def test_golden_training_run_fp64(name):
 
 @pytest.mark.parametrize("compat,dim,shape", [(False, 32, "small"), (True, 20, "small"), (False, 50, "small"),
                                                (False, 65, "tiny"), (True, 96, "tiny"), (False, 100, "tiny"),
-                                               (True, 100, "tiny"), (False, 128, "tiny")])
+                                               (True, 100, "tiny"), (False, 128, "tiny"), (True, 160, "tiny"),
+                                               (False, 260, "tiny")])
 def test_oracle_parity_with_transrnorm(compat, dim, shape):
     """dim <= 64: Mr rows in registers (transr_owner_reg_kernel); above: the
-    LDS-resident generic owner (engine_relowner.inc), K5's n = 100 included."""
+    LDS-resident generic owner (engine_relowner.inc), K5's n = 100 included;
+    above 137 the same owner on the matrix in L2 (the reference's --size has no
+    limit, common/args.cpp:71-74), 260 with four element chunks a lane."""
     ds = data.synthetic(shape, seed=4)
     kw = dict(rate=0.005 if shape == "small" else 0.01, margin=1.0, method=1, batches=25 if shape == "small" else 10)
     m = oracle_model("R", ds, dim, transr_compat=compat, **kw)
