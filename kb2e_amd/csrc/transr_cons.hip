@@ -14,6 +14,7 @@
 #include "kernels_transr_seq.hpp"
 #include "kernels_transr_chainw.hpp"
 #include "kernels_transr_chainwp.hpp"
+#include "kernels_transr_chainwv.hpp"
 #include "kernels_transr_chaing.hpp"
 #include "kernels_transr_pipe.hpp"
 #include "kernels_transr_wave.hpp"
@@ -94,11 +95,28 @@ const void* chainwp_fn(int n) {
     throw std::runtime_error("transRNorm pipelined wide chain kernel: no instantiation");
 }
 
+const void* chainwv_fn(int n) {
+    switch (wp_ks(n)) {
+        case 18: return (const void*)transr_cons_chain_wv_kernel<18>;
+        case 20: return (const void*)transr_cons_chain_wv_kernel<20>;
+        case 22: return (const void*)transr_cons_chain_wv_kernel<22>;
+        case 24: return (const void*)transr_cons_chain_wv_kernel<24>;
+        case 25: return (const void*)transr_cons_chain_wv_kernel<25>;
+    }
+    throw std::runtime_error("transRNorm pipelined wide chain kernel (V on the helpers): no instantiation");
+}
+
 // 64 < n <= 100: the pipelined wide chain (kernels_transr_chainwp.hpp);
 // KB2E_RPAR_CHAIN=lockstep keeps the eight-wave lockstep kernel (A/B)
 bool use_wpipe(int n) {
     const char* e = getenv("KB2E_RPAR_CHAIN");
     return n > 64 && n <= kWPMaxN && !(e && (std::string(e) == "lockstep" || std::string(e) == "wide"));
+}
+// and KB2E_RPAR_CHAIN=wv its variant with V = p K0 made by the helper waves
+// (kernels_transr_chainwv.hpp)
+bool use_wv(int n) {
+    const char* e = getenv("KB2E_RPAR_CHAIN");
+    return use_wpipe(n) && e && std::string(e) == "wv";
 }
 
 // KB2E_RPAR_CHAIN=serial: the unpipelined chain kernel (kernels_transr_seq.hpp)
@@ -133,10 +151,10 @@ bool cons_chainw_supported(int n) { return n >= 1 && n <= kWideMaxN; }
 size_t cons_chainw_setup(int n) {
     HIPCHK(hipFuncSetAttribute((const void*)transr_cons_da_rel_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)da_rel_lds(n)));
-    const bool wp = use_wpipe(n);
-    const size_t lds = wp ? chainwp_lds(n) : chainw_lds(n);
-    HIPCHK(hipFuncSetAttribute(wp ? chainwp_fn(n) : chainw_fn(n), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)lds));
+    const bool wp = use_wpipe(n), wv = use_wv(n);
+    const size_t lds = wv ? chainwv_lds(n) : wp ? chainwp_lds(n) : chainw_lds(n);
+    HIPCHK(hipFuncSetAttribute(wv ? chainwv_fn(n) : wp ? chainwp_fn(n) : chainw_fn(n),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     return lds;
 }
 
@@ -149,7 +167,8 @@ void cons_chainw_launch(const RParArgs& a, const RParBufs<double>& bf, size_t ld
     // one workgroup per relation, most frequent first (those absent from the batch exit)
     const int grid = a.nr;
     // (the LDS size was chosen by cons_chainw_setup under the same switch)
-    if (use_wpipe(a.n)) HIPCHK(hipLaunchKernel(chainwp_fn(a.n), dim3(grid), dim3(kWPThreads), args, lds, stream));
+    if (use_wv(a.n)) HIPCHK(hipLaunchKernel(chainwv_fn(a.n), dim3(grid), dim3(kWPThreads), args, lds, stream));
+    else if (use_wpipe(a.n)) HIPCHK(hipLaunchKernel(chainwp_fn(a.n), dim3(grid), dim3(kWPThreads), args, lds, stream));
     else HIPCHK(hipLaunchKernel(chainw_fn(a.n), dim3(grid), dim3(kWideThreads), args, lds, stream));
     // the pair records: a workgroup per relation, its final matrix staged once
     // (KB2E_RPAR_DA=wave: a wave a record over the whole record array, W from L2; A/B)

@@ -185,3 +185,36 @@ def test_k5_full_size_compat_energy(k5):
         _check_rows(ent, rel, w, *cur, ids, act, ds.num_entities, ds.num_relations)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("chain", ["wv", "lockstep"])
+def test_k5_chain_kernels_agree(k5, chain, monkeypatch):
+    """One full-size batch (compat energy) through each transRNorm chain kernel
+    at n = 100 against the default one: the same pairs in the same order
+    against the same matrices, so the tables agree to rounding (the kernels sum
+    V = p K0 and the projections in different orders)."""
+    ds, ent, rel, stream, B = k5
+    w = np.ascontiguousarray(np.broadcast_to(np.eye(N), (ds.num_relations, N, N)))
+    out = {}
+    for name in ("default", chain):
+        if name == "default":
+            monkeypatch.delenv("KB2E_RPAR_CHAIN", raising=False)
+        else:
+            monkeypatch.setenv("KB2E_RPAR_CHAIN", name)
+        eng = Engine("R", N, ds.num_entities, ds.num_relations, rate=0.001, method=1, distance=0,
+                     batches=BATCHES, seed=SEED, schedule="parallel", transr_compat=True)
+        try:
+            eng.upload_triples(ds.train)
+            eng.upload_params(ent, rel, w)
+            eng.train_batches(1)
+            eng.synchronize()
+            out[name] = (eng.take_stats(), eng.download_params())
+        finally:
+            eng.close()
+    (l0, a0), p0 = out["default"]
+    (l1, a1), p1 = out[chain]
+    assert a0 == a1 and l0 == l1  # the hinge pass comes before the chain
+    for x0, x1 in zip(p0, p1):
+        assert np.abs(x1 - x0).max() < 1e-11
+    # the chain moved the hot relations' matrices (the comparison is not vacuous)
+    assert np.abs(p0[2] - w).max() > 1e-6

@@ -179,7 +179,7 @@ def test_transr_parallel_chain_windows(dim, compat, env, St, chain, monkeypatch)
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=compat)
 
 
-@pytest.mark.parametrize("chain", ["default", "lockstep"])
+@pytest.mark.parametrize("chain", ["default", "lockstep", "wv"])
 @pytest.mark.parametrize("dim,compat,mfma", [(100, True, False), (100, False, False), (72, True, True),
                                              (20, True, False), (88, False, True)])
 def test_transr_parallel_wide_chain_windows(dim, compat, mfma, chain, monkeypatch):
@@ -190,8 +190,8 @@ def test_transr_parallel_wide_chain_windows(dim, compat, mfma, chain, monkeypatc
     samples a batch (B = 3,000), so W_c, K0, the pipeline's pending W update and
     the held-back tail (the relation's last update) carry across windows; n = 20
     on the VALU path runs the lockstep kernel at one column tile either way."""
-    if chain == "lockstep":
-        monkeypatch.setenv("KB2E_RPAR_CHAIN", "lockstep")
+    if chain != "default":
+        monkeypatch.setenv("KB2E_RPAR_CHAIN", chain)
     _transr_vs_model(data.synthetic("small", seed=1), dim, 1, monkeypatch, St=2 if mfma else 8, compat=compat,
                      mfma=mfma, rate=0.001)
 
