@@ -226,6 +226,9 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
     // helpers: X = A W_c on their column tile (KS k-steps, B from the registers);
     // wave 4 also the chunk's Gram matrix A A^T (its B operand is its A operand),
     // wave 5 the cross Gram A A_c^T with the current chunk (Ac; none for a fresh chunk)
+    // The Gram matrices ride on waves 6 / 7 (NB = 7), off the walker's SIMD (wave w runs on
+    // SIMD w mod 4): 4% on the K5 line (KB2E_CONS_DBG bit 1: waves 4 / 5, A/B; same results)
+    const int gw = !(bf.dbg & 2) && NB >= 7 ? 6 : 4, cw = !(bf.dbg & 2) && NB >= 7 ? 7 : 5;
     auto x_tile = [&](const T* Ar, T* out, T* G, const T* Ac) {
         if (!own) return;
         typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
@@ -238,14 +241,14 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
 #pragma unroll
             for (int q = 0; q < 4; ++q) out[(kq + 4 * q) * LA + col] = acc[q];
         }
-        if (w == 4) {
+        if (w == gw) {
             typename M::acc_t ga = {T(0), T(0), T(0), T(0)};
 #pragma unroll
             for (int q = 0; q < KS; ++q) ga = M::mma(av[q], av[q], ga);
 #pragma unroll
             for (int q = 0; q < 4; ++q) G[(kq + 4 * q) * LG + l16] = ga[q];
         }
-        if (w == 5 && Ac) {  // the cross Gram with the current chunk's rows (the fold's dots)
+        if (w == cw && Ac) {  // the cross Gram with the current chunk's rows (the fold's dots)
             typename M::acc_t ca = {T(0), T(0), T(0), T(0)};
 #pragma unroll
             for (int q = 0; q < KS; ++q) ca = M::mma(av[q], Ac[l16 * LA + 4 * q + kq], ca);
@@ -355,47 +358,58 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
 #pragma unroll
                     for (int u = 0; u < KS; ++u) P[v * LA + h * KS + u] = x[u];
                 }
+                if (bf.dbg & 4) tick(7);  // (timing experiment: the pick and row store apart from V)
                 // a_j . a_v for every row, from the chunk's Gram matrix
                 const T dp = Gm[j * LG + v];
                 // V_c = sum_i p_v[i] K0[i][c], c = l and l + 64: 16-byte reads of K0's row
                 // pairs (consecutive lanes, consecutive pairs), p_v as broadcasts; the
                 // second column's reads are clamped, not branched (its lanes >= NC - 64
-                // discard the sums)
+                // read one address and discard the sums)
                 const T* pr = P + v * LA;
                 const double2* kp = (const double2*)K0;
                 const double2* pp2 = (const double2*)pr;
-                const int c1r = c1 < NC ? c1 : l;
+                const int c1r = c1 < NC ? c1 : NC - 1;  // (lanes past the columns: one broadcast address)
                 T va[4] = {T(0), T(0), T(0), T(0)}, vb[4] = {T(0), T(0), T(0), T(0)};
-                // software-pipelined: the next four rows' six 16-byte reads are in flight
-                // while the current four rows' FMAs run (one LDS round trip per two steps)
-                double2 cur[6], nxt[6];
-                auto ld6 = [&](int i2, double2 (&d)[6]) {
-                    d[0] = pp2[i2];
-                    d[1] = pp2[i2 + 1];
-                    d[2] = kp[i2 * NC + l];
-                    d[3] = kp[(i2 + 1) * NC + l];
-                    d[4] = kp[i2 * NC + c1r];
-                    d[5] = kp[(i2 + 1) * NC + c1r];
+                // software-pipelined over the NC / 2 row pairs: the reads of the next D pairs
+                // (three 16-byte reads a pair, 3 D <= 15 in flight: the LDS counter's range)
+                // are issued while the current pair's four FMAs run.  The slots rotate
+                // without copies and every condition is a compile-time one (a runtime one
+                // turns the slots into phi copies that wait for every read)
+                constexpr int NP2 = NC / 2, D = 4, NG = NP2 / D, REM = NP2 % D;
+                static_assert(NG >= 1, "a full group of pairs");
+                double2 bp[D], ba[D], bb[D];
+                auto ld = [&](int i, int t) {
+                    bp[t] = pp2[i];
+                    ba[t] = kp[i * NC + l];
+                    bb[t] = kp[i * NC + c1r];
                 };
-                auto fm6 = [&](const double2 (&d)[6]) {
-                    va[0] = fma(d[0].x, d[2].x, va[0]);
-                    va[1] = fma(d[0].y, d[2].y, va[1]);
-                    va[2] = fma(d[1].x, d[3].x, va[2]);
-                    va[3] = fma(d[1].y, d[3].y, va[3]);
-                    vb[0] = fma(d[0].x, d[4].x, vb[0]);
-                    vb[1] = fma(d[0].y, d[4].y, vb[1]);
-                    vb[2] = fma(d[1].x, d[5].x, vb[2]);
-                    vb[3] = fma(d[1].y, d[5].y, vb[3]);
+                auto fm = [&](int t) {  // (pair parity = t's: D even)
+                    const int e = (t & 1) * 2;
+                    va[e] = fma(bp[t].x, ba[t].x, va[e]);
+                    va[e + 1] = fma(bp[t].y, ba[t].y, va[e + 1]);
+                    vb[e] = fma(bp[t].x, bb[t].x, vb[e]);
+                    vb[e + 1] = fma(bp[t].y, bb[t].y, vb[e + 1]);
                 };
-                ld6(0, cur);
-#pragma unroll 2
-                for (int i2 = 2; i2 < NC / 2; i2 += 2) {  // (NC = 4 KS: whole steps of four rows)
-                    ld6(i2, nxt);
-                    fm6(cur);
 #pragma unroll
-                    for (int t = 0; t < 6; ++t) cur[t] = nxt[t];
+                for (int t = 0; t < D; ++t) ld(t, t);
+                // groups of D pairs, rolled (unrolled, the scheduler hoists every read and
+                // spills), each refill pinned right behind its slot's FMAs
+#pragma unroll 1
+                for (int g = 0; g + 1 < NG; ++g) {
+#pragma unroll
+                    for (int t = 0; t < D; ++t) {
+                        fm(t);
+                        ld((g + 1) * D + t, t);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
                 }
-                fm6(cur);
+#pragma unroll
+                for (int t = 0; t < D; ++t) {  // the last full group, refilling the remainder
+                    fm(t);
+                    if (t < REM) ld(NG * D + t, t);
+                }
+#pragma unroll
+                for (int t = 0; t < REM; ++t) fm(t);
                 const T V0 = (va[0] + va[1]) + (va[2] + va[3]);
                 const T V1 = c1 < NC ? (vb[0] + vb[1]) + (vb[2] + vb[3]) : T(0);
                 tick(13);
@@ -467,37 +481,14 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
         __syncthreads();
         fold(Pbuf, csz(0), 0, nullptr, nullptr);
         __syncthreads();
-        for (int k = 0; k < nch; ++k) {
-            const int cc = csz(k), cn = csz(k + 1);
-            const int ka = k % 3, kn = (k + 1) % 3, pc = k & 1;
-            const T* A = Abuf + ka * R * LA;
-            const T* An = Abuf + kn * R * LA;
-            T* P = Pbuf + pc * R * LA;
-            T* Pn = Pbuf + (pc ^ 1) * R * LA;
-            const T* Gm = Gbuf + pc * R * LG;
-            T* Gn = Gbuf + (pc ^ 1) * R * LG;
-            int* vl = vlist + pc * R;
-            ++n_chunks;
-            if (w == 0) {
-                walk(P, Gm, cc, k * R, vl);
-                tick(2);
-            } else {
-                apply_pending();  // chunk k - 1's
-                tick(10);
-                if (cn > 0 && !(bf.dbg & 1)) x_tile(An, Pn, Gn, A);
-                tick(11);
-            }
-            __syncthreads();  // B1: the walk's G rows and violators, X_{k+1}
-            tick(w == 0 ? 3 : 12);
-            if (bf.dbg & 1) {  // (timing experiment: the projections after the walk, not beside it)
-                if (w > 0 && cn > 0) x_tile(An, Pn, Gn, A);
-                __syncthreads();
-            }
+        // after B1, everyone: chunk k's debt noted for the helpers, the row slots, the fold
+        auto after_b1 = [&](int k) {
+            const int cn = csz(k + 1), pc = k & 1;
             const int nv = misc[2];
             pend_nv = nv;
             pend_par = pc;
             pend_pc = pc;
-            pend_ka = ka;
+            pend_ka = k % 3;
             pend_base = k * R;
             if (nv) changed = true;
             // chunk k + 2's rows into the slot chunk k - 1 left, chunk k + 3's in flight
@@ -505,10 +496,40 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
                 store_rows((k + 2) % 3);
                 if (k + 3 < nch) load_rows((k + 3) * R, (k + 3) * R + csz(k + 3));
             }
-            if (cn > 0) fold(Pn, cn, nv, P, vl);
-            tick(4);
-            __syncthreads();  // B2: P_{k+1} and its |p|^2
-            tick(5);
+            if (cn > 0) fold(Pbuf + (pc ^ 1) * R * LA, cn, nv, Pbuf + pc * R * LA, vlist + pc * R);
+        };
+        // one loop a role: the walker's holds no W_c fragment (zeros on wave 0, restated as
+        // such after its loop, so that they are not live across the walk)
+        if (w == 0) {
+            for (int k = 0; k < nch; ++k) {
+                const int pc = k & 1;
+                ++n_chunks;
+                walk(Pbuf + pc * R * LA, Gbuf + pc * R * LG, csz(k), k * R, vlist + pc * R);
+                tick(2);
+                __syncthreads();  // B1: the walk's G rows and violators, X_{k+1}
+                tick(3);
+                after_b1(k);
+                tick(4);
+                __syncthreads();  // B2: P_{k+1} and its |p|^2
+                tick(5);
+            }
+#pragma unroll
+            for (int q = 0; q < KS; ++q) bW[q] = T(0);
+        } else {
+            for (int k = 0; k < nch; ++k) {
+                const int cn = csz(k + 1), pc = k & 1;
+                ++n_chunks;
+                apply_pending();  // chunk k - 1's
+                tick(10);
+                if (cn > 0)
+                    x_tile(Abuf + ((k + 1) % 3) * R * LA, Pbuf + (pc ^ 1) * R * LA, Gbuf + (pc ^ 1) * R * LG,
+                           Abuf + (k % 3) * R * LA);
+                tick(11);
+                __syncthreads();  // B1
+                tick(12);
+                after_b1(k);
+                __syncthreads();  // B2
+            }
         }
         apply_pending();
         pend_nv = 0;

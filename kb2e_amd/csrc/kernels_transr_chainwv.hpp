@@ -87,7 +87,7 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wv_kernel(RParAr
     unsigned long long n_chunks = 0, n_vio = 0, n_rounds = 0, max_m = 0;
     // KB2E_RPAR_STATS (g_seq_stats 8..23; relations of >= 200 chunks also 24..39): thread 0
     // (walker) 0 prologue + K0, 1 window list, 2 walk, 3 B1 wait, 6 drain, 7 window flags,
-    // 8 tail, 9 write-back + records, 13 pick + row + request + V wait, 14 sums + rounds + g,
+    // 8 tail, 9 write-back + records, 5 pick + row + request, 13 V wait, 14 sums + rounds + g,
     // 15 later rows; thread 64 (helper wave 1) 10 debt, 11 X tile + sync, 12 rows + fold
     // until the walk ends + |p|^2, 4 B1 wait
     __shared__ unsigned long long ph[16];
@@ -257,9 +257,12 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wv_kernel(RParAr
             __builtin_amdgcn_s_sleep(1);
         }
     };
-    // helpers: X = A W_c on their column tile; wave 4 also the chunk's Gram matrix A A^T,
-    // wave 5 the cross Gram A A_c^T with the current chunk (none for a fresh chunk);
-    // the walker's requests answered between groups of five k-steps (P: its chunk)
+    // helpers: X = A W_c on their column tile; wave gw also the chunk's Gram matrix A A^T,
+    // wave cw the cross Gram A A_c^T with the current chunk (none for a fresh chunk);
+    // the walker's requests answered between groups of five k-steps (P: its chunk).
+    // (the Gram matrices on waves 6 / 7 at NB = 7, off the walker's SIMD; KB2E_CONS_DBG bit 1:
+    // waves 4 / 5, A/B; same results)
+    const int gw = !(bf.dbg & 2) && NB >= 7 ? 6 : 4, cw = !(bf.dbg & 2) && NB >= 7 ? 7 : 5;
     auto x_tile = [&](const T* Ar, T* out, T* G, const T* Ac, const T* P) {
         if (!own) return;
         typename M::acc_t acc = {T(0), T(0), T(0), T(0)};
@@ -270,8 +273,8 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wv_kernel(RParAr
             for (int q = q0; q < q0 + 5 && q < KS; ++q) {
                 const T av = Ar[l16 * LA + 4 * q + kq];
                 acc = M::mma(av, bW[q], acc);
-                if (w == 4) ga = M::mma(av, av, ga);
-                else if (w == 5 && Ac) ga = M::mma(av, Ac[l16 * LA + 4 * q + kq], ga);
+                if (w == gw) ga = M::mma(av, av, ga);
+                else if (w == cw && Ac) ga = M::mma(av, Ac[l16 * LA + 4 * q + kq], ga);
             }
             if (P) answer(P);
         }
@@ -279,11 +282,11 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wv_kernel(RParAr
 #pragma unroll
             for (int q = 0; q < 4; ++q) out[(kq + 4 * q) * LA + col] = acc[q];
         }
-        if (w == 4) {
+        if (w == gw) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) G[(kq + 4 * q) * LG + l16] = ga[q];
         }
-        if (w == 5 && Ac) {
+        if (w == cw && Ac) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) Cx[(kq + 4 * q) * LG + l16] = ga[q];
         }
@@ -417,6 +420,7 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wv_kernel(RParAr
                 const T aa = readlane_f(dp, v);  // |a_v|^2
                 T rpp = __builtin_amdgcn_rcp(pp);  // v_rcp_f64 and one Newton step
                 rpp = fma(fma(-pp, rpp, T(1)), rpp, rpp);
+                tick(5);
                 for (uint32_t sp = 0;
                      __hip_atomic_load(&vreq[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NB * vreqs; ++sp) {
                     if (sp > (1u << 24)) {

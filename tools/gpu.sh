@@ -12,7 +12,8 @@
 #   bash tools/gpu.sh hits     <tag>                        FB15k-shaped Hits@10 schedule parity, four configs
 #   bash tools/gpu.sh k5       <tag>                        n > 64 parity tests, K5 tests, the K5 line
 #   bash tools/gpu.sh final    <tag>                        suite + default line + K5 line
-#   bash tools/gpu.sh k5stats  <tag> <chain> [chain ...]      K5 chain phase counters per KB2E_RPAR_CHAIN ("-" = unset)
+#   bash tools/gpu.sh k5stats  <tag> <chain> [chain ...]      K5 chain phase counters per KB2E_RPAR_CHAIN ("-" = unset;
+#                                                           CFG=<config> for another bench config)
 #   bash tools/gpu.sh timeline <tag>                        kernel timeline of the driver-style line (K=20)
 # (ab: AB_EPOCH=1 also times the whole epoch and epoch 50, e.g. the TransH gate sweep
 #  AB_EPOCH=1 bash tools/gpu.sh ab gate transh_fb15k KB2E_HPAR_ORTH_MIN 0 16 64 256)
@@ -55,7 +56,7 @@ case "$CMD" in
   k5stats)  # the chain kernels' phase counters (KB2E_RPAR_STATS) on the K5 line, per KB2E_RPAR_CHAIN value
     for V in "$@"; do
       if [ "$V" = "-" ]; then unset KB2E_RPAR_CHAIN; else export KB2E_RPAR_CHAIN=$V; fi
-      KB2E_RPAR_STATS=1 bench_run "st_$V" 300 --config transr_k5 --only --no-cpu-baseline --no-epoch --steps 10 --warmup 2 || exit 1
+      KB2E_RPAR_STATS=1 bench_run "st_$V" 300 --config "${CFG:-transr_k5}" --only --no-cpu-baseline --no-epoch --steps 10 --warmup 2 || exit 1
       grep "hot relations" "$OUT/st_$V.err" | tail -1 | sed 's/.*hot relations/hot/' | cut -c1-400
     done ;;
   timeline)
