@@ -154,8 +154,9 @@ struct kb2e_ctx {
     DevBuf hpar_orth;                      // PARALLEL TransH: orthogonality flags per sample
     DevBuf hpar_tag;                       // PARALLEL TransH: per entity, the relations its flagged pairs have
     uint32_t hpar_stamp = 0;
-    DevBuf hpar_count;                     // PARALLEL TransH: flagged samples of the last two batches
+    DevBuf hpar_count;                     // PARALLEL TransH: normOrth iterations of the last two batches
     uint32_t hpar_orth_min = 0;            // ... from which normOrth takes the relation pass
+    int32_t hpar_orth_q = 0;               // the one-wave pass's second-sweep queue (kOrthQ)
     // PARALLEL schedule: per-event records in sorted order (kernels_transe.hpp EventRecs)
     DevBuf ev_iota, ev_slot_sorted, ev_inv, seg_row, ev_meta, ev_words;
     // PARALLEL TransR (kernels_transr_parallel.hpp)
@@ -1147,6 +1148,8 @@ void setup_epoch_buffers(kb2e_ctx* c) {
         memset_sync(c->hpar_count.p, 0, c->hpar_count.bytes);
         const char* om = getenv("KB2E_HPAR_ORTH_MIN");  // tests: 0 always, a large value never
         c->hpar_orth_min = om ? (uint32_t)std::max(0, atoi(om)) : kOrthRelMin;
+        const char* oq = getenv("KB2E_HPAR_ORTH_Q");  // tests: 0 lists the second sweep's flags again
+        c->hpar_orth_q = oq ? std::max(0, std::min(kOrthQ, atoi(oq))) : kOrthQ;
         c->hpar_tag.alloc((size_t)c->cfg.num_entities * 8);  // zeroed: stamp 0 is never a batch's
         c->rpar_St = 1 << 30;  // build_transr_tiles(c, false): relation segment ranges only
         c->rpar_ntiles.alloc((size_t)(nkeys + 1) * 4);

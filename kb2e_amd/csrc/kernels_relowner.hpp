@@ -323,12 +323,14 @@ __global__ __launch_bounds__(256) void transh_score_kernel(HScoreArgs<T> a, Even
 }
 
 // common/utils.cpp:79-111 norm(a, b, rate) on registers, with the
-// reference's running `sum` (never reset between iterations).
+// reference's running `sum` (never reset between iterations).  Returns the
+// iterations run (the test included; wave-uniform).
 template <typename T, int CH>
-__device__ __forceinline__ void orth_norm(RowReg<T, CH>& A, RowReg<T, CH>& Bv, int n, T rate) {
+__device__ __forceinline__ int orth_norm(RowReg<T, CH>& A, RowReg<T, CH>& Bv, int n, T rate) {
     Bv.norm(n, false);
     T sum = T(0);
-    for (int it = 0; it < 1 << 20; ++it) {
+    int it = 0;
+    for (; it < 1 << 20; ++it) {
         sum += Bv.sumsq();
         sum = sqrt(sum);
 #pragma unroll
@@ -353,6 +355,7 @@ __device__ __forceinline__ void orth_norm(RowReg<T, CH>& A, RowReg<T, CH>& Bv, i
             }
     }
     Bv.norm(n, false);
+    return it + 1;
 }
 
 

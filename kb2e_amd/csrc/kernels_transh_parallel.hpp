@@ -47,11 +47,14 @@ struct HParArgs {
     uint8_t* orth_mask;       // [B] violating (update, row) pairs of each sample, bits u * 3 + {r, h, t}
     unsigned long long* ent_tag;  // [ne] stamp << 32 | multi << 31 | relation of the entity's flagged pairs
     uint32_t stamp;           // this batch's tag stamp (never 0)
-    // normOrth's relation pass runs when the previous batch flagged >= orth_rel_min samples
-    // (few flagged pairs: the one-wave pass alone is cheaper); counts alternate by batch
-    uint32_t* orth_count_cur;   // this batch's flagged samples (check kernel)
-    uint32_t* orth_count_prev;  // the previous batch's (read by the relation pass, then zeroed)
+    // normOrth's relation pass runs when the previous batch's normOrth work (its loop
+    // iterations over both passes, a wave-serial step each) was >= orth_rel_min (little
+    // work: the one-wave pass alone is cheaper than a launch over the relations); the
+    // work counts alternate by batch
+    uint32_t* orth_work_cur;    // this batch's iterations (relation and one-wave passes)
+    uint32_t* orth_work_prev;   // the previous batch's (read by the relation pass, then zeroed)
     uint32_t orth_rel_min;
+    int32_t orth_q;             // second-sweep queue capacity (kOrthQ; KB2E_HPAR_ORTH_Q for the tests)
 };
 
 // The flagged entity rows' relations this batch: the first relation a row is
@@ -208,7 +211,6 @@ __global__ __launch_bounds__(256) void transh_orth_check_kernel(HParArgs<T> a) {
     }
     if (l == 0) {
         a.orth_mask[kk] = (uint8_t)mask;
-        if (mask) atomicAdd(a.orth_count_cur, 1u);
         const int ids[6] = {r, h, t, r, nh, nt};
         for (int q = 1; q < 6; ++q)
             if (q != 3 && ((mask >> q) & 1u)) orth_tag_entity(a, ids[q], r);
@@ -224,8 +226,8 @@ __global__ __launch_bounds__(256) void transh_orth_check_kernel(HParArgs<T> a) {
 // relation (the reference reloads what it just stored), and a store is drained
 // only before a later load of the same row (PendingRows).
 constexpr int kOrthWords = 4;  // 8-byte flag words per lane per pass
-// flagged samples of the previous batch from which normOrth takes the relation pass
-// (KB2E_HPAR_ORTH_MIN; oracle/parallel.py ORTH_REL_MIN)
+// normOrth iterations of the previous batch from which normOrth takes the relation pass
+// (KB2E_HPAR_ORTH_MIN; a schedule choice only, the result is the same either way)
 constexpr uint32_t kOrthRelMin = 64;
 
 // Rows stored by this wave and not yet drained: a load of one of them waits
@@ -256,96 +258,145 @@ struct PendingRows {
 // it, this wave does them, in sample order -- the same result bit for bit, since
 // the relations' own pairs touch disjoint rows and normals (their interleaving
 // does not matter, only each relation's sample order).  So the gate on the
-// previous batch's flagged count (kOrthRelMin) is a schedule choice only.
+// previous batch's normOrth work (kOrthRelMin) is a schedule choice only.
+//
+// The first sweep queues the samples with shared rows (their ids and those rows'
+// bits, in sample order) in LDS, so the second runs from the queue without
+// listing the flags and fetching the ids again; past kOrthQ queued samples it
+// lists them again.
+constexpr int kOrthQ = 512;
+
 template <typename T, int CH>
 __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
     __shared__ int list[8 * kWave * kOrthWords];
+    __shared__ int queue[6][kOrthQ];  // second sweep: bits, r, h, t, h', t'
     const int l = lane_id();
     RowReg<T, CH> W;
     int wid = -1;
     PendingRows pend;
-    for (int sweep = 0; sweep < 2; ++sweep)
-    for (int base = 0; base < a.B; base += 8 * kWave * kOrthWords) {
-        uint64_t word[kOrthWords];
-#pragma unroll
-        for (int wi = 0; wi < kOrthWords; ++wi) {  // orth_mask is zero past B up to a multiple of 512
-            const int off = base + 8 * (wi * kWave + l);
-            word[wi] = off < a.B ? *reinterpret_cast<const uint64_t*>(a.orth_mask + off) : 0ull;
-        }
-        int count = 0;
-#pragma unroll
-        for (int wi = 0; wi < kOrthWords; ++wi) {  // sample order: word, lane, byte
-            int mine = 0;
-#pragma unroll
-            for (int by = 0; by < 8; ++by) mine += ((word[wi] >> (8 * by)) & 0xffu) != 0;
-            int pre = mine;  // inclusive scan over the lanes
-#pragma unroll
-            for (int d = 1; d < kWave; d <<= 1) {
-                const int v = __shfl_up(pre, d);
-                if (l >= d) pre += v;
+    uint32_t work = 0;  // normOrth iterations (the next batch's gate)
+    int nq = 0;         // samples queued for the second sweep (> kOrthQ: list them again)
+    // one sample's flagged rows (bits eb over r, h, t, -, h', t') against w_r, in row order
+    auto fix_sample = [&](uint32_t eb, const int (&ids)[6]) {
+        const int er = ids[0];
+        if (er != wid) {  // w_r: kept in registers while consecutive samples share the relation
+            if (wid >= 0) {
+                row_store_sc1(W, a.w + (int64_t)wid * a.ld, a.n);
+                pend.add(a.nr + wid);
             }
-            int pos = count + pre - mine;
-#pragma unroll
-            for (int by = 0; by < 8; ++by)
-                if (((word[wi] >> (8 * by)) & 0xffu) != 0) list[pos++] = base + 8 * (wi * kWave + l) + by;
-            count += __shfl(pre, kWave - 1);
+            pend.before_load(a.nr + er);
+            row_load_sc1(W, a.w + (int64_t)er * a.ld, a.n);
+            wid = er;
         }
-        wave_lds_sync();
-        for (int g = 0; g < count; g += kWave) {
-            int k2 = -1, r = 0, h = 0, t = 0, nh = 0, nt = 0, bits = 0;
-            if (g + l < count) {  // this lane's list entry: ids from the sample stream
-                k2 = list[g + l];
-                const int i0 = a.si[k2], j = a.sj[k2];
-                const bool sd = a.side[k2];
-                bits = a.orth_mask[k2];
-                h = a.heads[i0];
-                t = a.tails[i0];
-                r = a.rels[i0];
-                nh = sd ? h : j;
-                nt = sd ? j : t;
-                const int eid[6] = {r, h, t, r, nh, nt};
+        for (int q = 0; q < 6; ++q) {
+            if (!((eb >> q) & 1u)) continue;
+            const bool isrel = q == 0 || q == 3;
+            T* row = (isrel ? a.rel : a.ent) + (int64_t)ids[q] * a.ld;
+            // ids: relations [0, nr), w rows [nr, 2 nr), entities from 2 nr
+            const int key = isrel ? ids[q] : 2 * a.nr + ids[q];
+            RowReg<T, CH> A;
+            pend.before_load(key);
+            row_load_sc1(A, row, a.n);
+            work += (uint32_t)orth_norm<T, CH>(A, W, a.n, (T)a.lr);
+            row_store_sc1(A, row, a.n);
+            pend.add(key);
+        }
+    };
+    // a sweep over the flag words, samples in order (sweep 1 only when the queue overflowed)
+    auto sweep_flags = [&](int sweep) {
+        for (int base = 0; base < a.B; base += 8 * kWave * kOrthWords) {
+            uint64_t word[kOrthWords];
+#pragma unroll
+            for (int wi = 0; wi < kOrthWords; ++wi) {  // orth_mask is zero past B up to a multiple of 512
+                const int off = base + 8 * (wi * kWave + l);
+                word[wi] = off < a.B ? *reinterpret_cast<const uint64_t*>(a.orth_mask + off) : 0ull;
+            }
+            int count = 0;
+#pragma unroll
+            for (int wi = 0; wi < kOrthWords; ++wi) {  // sample order: word, lane, byte
+                int mine = 0;
+#pragma unroll
+                for (int by = 0; by < 8; ++by) mine += ((word[wi] >> (8 * by)) & 0xffu) != 0;
+                int pre = mine;  // inclusive scan over the lanes
+#pragma unroll
+                for (int d = 1; d < kWave; d <<= 1) {
+                    const int v = __shfl_up(pre, d);
+                    if (l >= d) pre += v;
+                }
+                int pos = count + pre - mine;
+#pragma unroll
+                for (int by = 0; by < 8; ++by)
+                    if (((word[wi] >> (8 * by)) & 0xffu) != 0) list[pos++] = base + 8 * (wi * kWave + l) + by;
+                count += __shfl(pre, kWave - 1);
+            }
+            wave_lds_sync();
+            for (int g = 0; g < count; g += kWave) {
+                int k2 = -1, bits = 0;
+                int eid[6] = {0, 0, 0, 0, 0, 0};
                 uint32_t sh = 0;  // the entity rows several relations flagged (second sweep)
+                if (g + l < count) {  // this lane's list entry: ids from the sample stream
+                    k2 = list[g + l];
+                    const int i0 = a.si[k2], j = a.sj[k2];
+                    const bool sd = a.side[k2];
+                    bits = a.orth_mask[k2];
+                    const int h = a.heads[i0], t = a.tails[i0], r = a.rels[i0];
+                    eid[0] = r;
+                    eid[1] = h;
+                    eid[2] = t;
+                    eid[3] = r;
+                    eid[4] = sd ? h : j;
+                    eid[5] = sd ? j : t;
 #pragma unroll
-                for (int q = 1; q < 6; ++q)
-                    if (q != 3 && ((bits >> q) & 1) && orth_shared(a, eid[q])) sh |= 1u << q;
-                bits = sweep == 0 ? bits & (int)~sh : (int)sh;
-            }
-            const int ng = min(kWave, count - g);
-            for (int e = 0; e < ng; ++e) {
-                const uint32_t eb = (uint32_t)readlane_i32(bits, e);
-                if (eb == 0) continue;  // (the other sweep's pairs)
-                const int er = readlane_i32(r, e);
-                const int ids[6] = {er, readlane_i32(h, e), readlane_i32(t, e), er, readlane_i32(nh, e),
-                                    readlane_i32(nt, e)};
-                if (er != wid) {  // w_r: kept in registers while consecutive samples share the relation
-                    if (wid >= 0) {
-                        row_store_sc1(W, a.w + (int64_t)wid * a.ld, a.n);
-                        pend.add(a.nr + wid);
+                    for (int q = 1; q < 6; ++q)
+                        if (q != 3 && ((bits >> q) & 1) && orth_shared(a, eid[q])) sh |= 1u << q;
+                    bits = sweep == 0 ? bits & (int)~sh : (int)sh;
+                }
+                if (sweep == 0) {  // the shared rows' samples queued for the second sweep, in order
+                    const uint64_t qm = __ballot(sh != 0);
+                    const int qp = nq + __builtin_popcountll(qm & ((1ull << l) - 1ull));
+                    if (sh != 0 && qp < a.orth_q) {
+                        queue[0][qp] = (int)sh;
+                        queue[1][qp] = eid[0];
+                        queue[2][qp] = eid[1];
+                        queue[3][qp] = eid[2];
+                        queue[4][qp] = eid[4];
+                        queue[5][qp] = eid[5];
                     }
-                    pend.before_load(a.nr + er);
-                    row_load_sc1(W, a.w + (int64_t)er * a.ld, a.n);
-                    wid = er;
+                    nq += __builtin_popcountll(qm);
                 }
-                for (int q = 0; q < 6; ++q) {
-                    if (!((eb >> q) & 1u)) continue;
-                    const bool isrel = q == 0 || q == 3;
-                    T* row = (isrel ? a.rel : a.ent) + (int64_t)ids[q] * a.ld;
-                    // ids: relations [0, nr), w rows [nr, 2 nr), entities from 2 nr
-                    const int key = isrel ? ids[q] : 2 * a.nr + ids[q];
-                    RowReg<T, CH> A;
-                    pend.before_load(key);
-                    row_load_sc1(A, row, a.n);
-                    orth_norm<T, CH>(A, W, a.n, (T)a.lr);
-                    row_store_sc1(A, row, a.n);
-                    pend.add(key);
+                const int ng = min(kWave, count - g);
+                for (int e = 0; e < ng; ++e) {
+                    const uint32_t eb = (uint32_t)readlane_i32(bits, e);
+                    if (eb == 0) continue;  // (the other sweep's pairs)
+                    const int er = readlane_i32(eid[0], e);
+                    const int ids[6] = {er, readlane_i32(eid[1], e), readlane_i32(eid[2], e), er,
+                                        readlane_i32(eid[4], e), readlane_i32(eid[5], e)};
+                    fix_sample(eb, ids);
                 }
             }
+            wave_lds_sync();
         }
+    };
+    sweep_flags(0);
+    if (nq <= a.orth_q) {
         wave_lds_sync();
+        for (int e = 0; e < nq; ++e) {
+            const int er = __builtin_amdgcn_readfirstlane(queue[1][e]);
+            const int ids[6] = {er, __builtin_amdgcn_readfirstlane(queue[2][e]),
+                                __builtin_amdgcn_readfirstlane(queue[3][e]), er,
+                                __builtin_amdgcn_readfirstlane(queue[4][e]),
+                                __builtin_amdgcn_readfirstlane(queue[5][e])};
+            fix_sample((uint32_t)__builtin_amdgcn_readfirstlane(queue[0][e]), ids);
+        }
+    } else {
+        sweep_flags(1);
     }
     if (wid >= 0) row_store_sc1(W, a.w + (int64_t)wid * a.ld, a.n);
     drain_stores();
-    if (l == 0) *a.orth_count_prev = 0;  // read by this batch's relation pass; the next batch counts into it
+    if (l == 0) {
+        atomicAdd(a.orth_work_cur, work);
+        *a.orth_work_prev = 0;  // read by this batch's relation pass; the next batch counts into it
+    }
 }
 
 // normOrth, first pass (oracle/parallel.py transh_parallel_batches): one wave per
@@ -356,9 +407,8 @@ __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
 // several relations flagged.  The relations' passes touch disjoint rows.
 template <typename T, int CH>
 __global__ __launch_bounds__(256) void transh_orth_rel_kernel(HParArgs<T> a) {
-    // few flagged pairs in the previous batch: leave every pair to the one-wave pass
-    // (the same rule in oracle/parallel.py transh_parallel_batches)
-    if (*a.orth_count_prev < a.orth_rel_min) return;
+    // little normOrth work in the previous batch: leave every pair to the one-wave pass
+    if (*a.orth_work_prev < a.orth_rel_min) return;
     const int s = a.rel_begin[a.batch] + (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
     if (s >= a.batch_seg[a.batch + 1]) return;
     const int l = lane_id();
@@ -366,6 +416,7 @@ __global__ __launch_bounds__(256) void transh_orth_rel_kernel(HParArgs<T> a) {
     const int r = a.seg_row[s] - a.ne;
     RowReg<T, CH> W;
     bool have_w = false;
+    uint32_t work = 0;  // normOrth iterations (the next batch's gate)
     PendingRows pend;  // a row stored earlier is drained before it is loaded again
     for (int base = p0; base < p1; base += kWave) {
         // lane-parallel: this lane's sample (an active sample's first update event),
@@ -416,7 +467,7 @@ __global__ __launch_bounds__(256) void transh_orth_rel_kernel(HParArgs<T> a) {
                 RowReg<T, CH> A;
                 pend.before_load(key);
                 row_load_sc1(A, row, a.n);
-                orth_norm<T, CH>(A, W, a.n, (T)a.lr);
+                work += (uint32_t)orth_norm<T, CH>(A, W, a.n, (T)a.lr);
                 row_store_sc1(A, row, a.n);
                 pend.add(key);
             }
@@ -424,6 +475,7 @@ __global__ __launch_bounds__(256) void transh_orth_rel_kernel(HParArgs<T> a) {
     }
     if (have_w) row_store_sc1(W, a.w + (int64_t)r * a.ld, a.n);
     drain_stores();
+    if (work && l == 0) atomicAdd(a.orth_work_cur, work);
 }
 
 

@@ -263,8 +263,10 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
         const T* Pp = Pbuf + pend_pc * R * LA;
         const T* Ap = Abuf + pend_ka * R * LA;
         const int* vl = vlist + pend_par * R;
+        // the violators' rows as wave-uniform values (one LDS read for all of them)
+        const int vmine = l < pend_nv ? vl[l] : 0;
         for (int k = 0; k < pend_nv; ++k) {
-            const int v = vl[k];
+            const int v = __builtin_amdgcn_readlane(vmine, k);
             const T gl = col < NC ? -lr * Pp[v * LA + col] : T(0);
 #pragma unroll
             for (int q = 0; q < KS; ++q) bW[q] = fma(Ap[v * LA + 4 * q + kq], gl, bW[q]);

@@ -386,13 +386,16 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
         const T* Pp = Pbuf + pend_pc * R * L;
         const T* Ap = Abuf + pend_ka * R * L;
         const int* vl = vlist + pend_par * R;
+        // the violators' rows as wave-uniform values (one LDS read for all of them), so that
+        // the next violator's reads need not wait for this one's list entry
+        const int vmine = l < pend_nv ? vl[l] : 0;
 #pragma unroll
         for (int si = 0; si < NSW; ++si) {
             const int cb = hw + 3 * si;
             if (cb >= NB) continue;
             const int c = cb * 16 + l16;
             for (int k = 0; k < pend_nv; ++k) {
-                const int v = vl[k];
+                const int v = __builtin_amdgcn_readlane(vmine, k);
                 const T gl = -lr * Pp[v * L + c];
 #pragma unroll
                 for (int s = 0; s < KS; ++s) reg[si * KS + s] = fma(Ap[v * L + 4 * s + kq], gl, reg[si * KS + s]);

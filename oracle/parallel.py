@@ -361,7 +361,7 @@ def transh_orth_order(samples, flags, ids, r):
     return out
 
 
-ORTH_REL_MIN = 64  # kernels_transh_parallel.hpp kOrthRelMin
+ORTH_REL_MIN = 64  # kernels_transh_parallel.hpp kOrthRelMin (normOrth iterations; a schedule choice only)
 
 
 def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, rate, margin=1.0, state=None,
@@ -378,11 +378,11 @@ def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
     (common/utils.cpp:79-111): first the pairs whose row only their relation
     touches (per relation, samples in order), then the entity rows flagged
     under several relations (samples in order).  The GPU runs the first pass as a
-    wave per relation when the previous batch flagged at least `orth_rel_min`
-    samples and on its one wave otherwise, with the same result (the relations'
-    own pairs touch disjoint rows and normals), so the gate does not enter the
-    model; `state` carries the previous batch's flagged-sample count (the
-    engine's, across epochs) for the tests that check both kernels ran.
+    wave per relation when the previous batch's normOrth work (loop iterations)
+    was at least `orth_rel_min` and on its one wave otherwise, with the same
+    result (the relations' own pairs touch disjoint rows and normals), so the
+    gate does not enter the model; `state` records the flagged-sample counts for
+    the tests.
     """
     from oracle import orc
 
@@ -437,9 +437,9 @@ def transh_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
             flags.append([q for q in range(6) if rows[q] is not None and W[r[kk]] @ rows[q][0][rows[q][1]] > 0.1])
         ids = {kk: (r[kk], h[kk], t[kk], None, nh[kk], nt[kk]) for kk in a}
         # the two-pass order whichever kernel runs it: the gate on the previous batch's
-        # flagged count (orth_rel_min) picks the relation pass or the one-wave pass's
+        # normOrth work (orth_rel_min) picks the relation pass or the one-wave pass's
         # first sweep, which give the same result (kernels_transh_parallel.hpp
-        # transh_orth_fix_kernel); it is recorded for the tests, not applied
+        # transh_orth_fix_kernel); not applied here
         order = transh_orth_order(list(a), flags, ids, r)
         state["orth_flagged"] = sum(1 for fl in flags if fl)
         if "flag_hist" in state:  # tests: the per-batch counts the gate saw

@@ -396,10 +396,21 @@ def test_transh_parallel(dim):
 
 @pytest.mark.parametrize("orth_min", [0, 1 << 30, 8])
 def test_transh_parallel_orth_gate(orth_min, monkeypatch):
-    """normOrth's relation pass runs only when the previous batch flagged at least
-    KB2E_HPAR_ORTH_MIN samples (0: always; huge: never, the one-wave pass takes
-    the relations' own pairs in its first sweep; 8: batches of both kinds on the
-    tiny set).  The result does not depend on it: one CPU model for all three."""
+    """normOrth's relation pass runs only when the previous batch's normOrth work
+    was at least KB2E_HPAR_ORTH_MIN loop iterations (0: always; huge: never, the
+    one-wave pass takes the relations' own pairs in its first sweep; 8: batches
+    of both kinds on the tiny set).  The result does not depend on it: one CPU
+    model for all three."""
+    monkeypatch.setenv("KB2E_HPAR_ORTH_MIN", str(orth_min))
+    _transh_vs_model(tiny(), 20, 2, orth_min=orth_min)
+
+
+@pytest.mark.parametrize("orth_min", [0, 1 << 30])
+def test_transh_parallel_orth_requeue(orth_min, monkeypatch):
+    """KB2E_HPAR_ORTH_Q=0: the one-wave pass's second sweep (the entity rows several
+    relations flagged) lists the flags again instead of running from its LDS queue
+    (the form past 512 queued samples); the same CPU model."""
+    monkeypatch.setenv("KB2E_HPAR_ORTH_Q", "0")
     monkeypatch.setenv("KB2E_HPAR_ORTH_MIN", str(orth_min))
     _transh_vs_model(tiny(), 20, 2, orth_min=orth_min)
 
