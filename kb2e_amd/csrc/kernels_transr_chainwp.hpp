@@ -263,13 +263,25 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
         const T* Pp = Pbuf + pend_pc * R * LA;
         const T* Ap = Abuf + pend_ka * R * LA;
         const int* vl = vlist + pend_par * R;
-        // the violators' rows as wave-uniform values (one LDS read for all of them)
+        // the violators' rows as wave-uniform values (one LDS read for all of them); the
+        // next violator's reads in flight while this one's FMAs run
         const int vmine = l < pend_nv ? vl[l] : 0;
-        for (int k = 0; k < pend_nv; ++k) {
+        T an[KS], gn = T(0);
+        auto ldv = [&](int k) {
             const int v = __builtin_amdgcn_readlane(vmine, k);
-            const T gl = col < NC ? -lr * Pp[v * LA + col] : T(0);
 #pragma unroll
-            for (int q = 0; q < KS; ++q) bW[q] = fma(Ap[v * LA + 4 * q + kq], gl, bW[q]);
+            for (int q = 0; q < KS; ++q) an[q] = Ap[v * LA + 4 * q + kq];
+            gn = col < NC ? -lr * Pp[v * LA + col] : T(0);
+        };
+        ldv(0);
+        for (int k = 0; k < pend_nv; ++k) {
+            T ac[KS];
+#pragma unroll
+            for (int q = 0; q < KS; ++q) ac[q] = an[q];
+            const T gl = gn;
+            if (k + 1 < pend_nv) ldv(k + 1);
+#pragma unroll
+            for (int q = 0; q < KS; ++q) bW[q] = fma(ac[q], gl, bW[q]);
         }
         for (int k = kq; k < pend_nv; k += 4) {
             const int v = vl[k];

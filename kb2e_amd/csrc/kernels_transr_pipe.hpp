@@ -386,21 +386,43 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
         const T* Pp = Pbuf + pend_pc * R * L;
         const T* Ap = Abuf + pend_ka * R * L;
         const int* vl = vlist + pend_par * R;
-        // the violators' rows as wave-uniform values (one LDS read for all of them), so that
-        // the next violator's reads need not wait for this one's list entry
+        // the violators' rows as wave-uniform values (one LDS read for all of them); a
+        // violator's a row serves every slice, and the next violator's reads are in flight
+        // while this one's FMAs run (per element the same order of updates)
         const int vmine = l < pend_nv ? vl[l] : 0;
+        T an[KS], gn[NSW];
+        auto ldv = [&](int k) {
+            const int v = __builtin_amdgcn_readlane(vmine, k);
+#pragma unroll
+            for (int s = 0; s < KS; ++s) an[s] = Ap[v * L + 4 * s + kq];
+#pragma unroll
+            for (int si = 0; si < NSW; ++si) {
+                const int cb = hw + 3 * si;
+                gn[si] = cb < NB ? -lr * Pp[v * L + cb * 16 + l16] : T(0);
+            }
+        };
+        const int nvu = (bf.dbg & 16) ? 0 : pend_nv;  // (dbg 16, 8: timing experiments)
+        if (nvu > 0) ldv(0);
+        for (int k = 0; k < nvu; ++k) {
+            T ac[KS], gc[NSW];
+#pragma unroll
+            for (int s = 0; s < KS; ++s) ac[s] = an[s];
+#pragma unroll
+            for (int si = 0; si < NSW; ++si) gc[si] = gn[si];
+            if (k + 1 < nvu) ldv(k + 1);
+#pragma unroll
+            for (int si = 0; si < NSW; ++si)
+                if (hw + 3 * si < NB) {
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) reg[si * KS + s] = fma(ac[s], gc[si], reg[si * KS + s]);
+                }
+        }
 #pragma unroll
         for (int si = 0; si < NSW; ++si) {
             const int cb = hw + 3 * si;
             if (cb >= NB) continue;
             const int c = cb * 16 + l16;
-            for (int k = 0; k < pend_nv; ++k) {
-                const int v = __builtin_amdgcn_readlane(vmine, k);
-                const T gl = -lr * Pp[v * L + c];
-#pragma unroll
-                for (int s = 0; s < KS; ++s) reg[si * KS + s] = fma(Ap[v * L + 4 * s + kq], gl, reg[si * KS + s]);
-            }
-            for (int k = kq; k < pend_nv; k += 4) {
+            for (int k = kq; k < ((bf.dbg & 8) ? 0 : pend_nv); k += 4) {
                 const int v = vl[k];
                 const int sl = ps[pend_base + v];
                 T* dst = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
