@@ -263,44 +263,103 @@ struct PendingRows {
 // The first sweep queues the samples with shared rows (their ids and those rows'
 // bits, in sample order) in LDS, so the second runs from the queue without
 // listing the flags and fetching the ids again; past kOrthQ queued samples it
-// lists them again.
+// lists them again.  Each group of samples runs pair by pair with the next pair's
+// rows loaded ahead (process_group).
 constexpr int kOrthQ = 512;
 
 template <typename T, int CH>
 __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
     __shared__ int list[8 * kWave * kOrthWords];
     __shared__ int queue[6][kOrthQ];  // second sweep: bits, r, h, t, h', t'
+    __shared__ int plist[kWave * 5];  // a group's (row, w_r) pairs in order: entry << 3 | row
     const int l = lane_id();
     RowReg<T, CH> W;
     int wid = -1;
     PendingRows pend;
     uint32_t work = 0;  // normOrth iterations (the next batch's gate)
-    int nq = 0;         // samples queued for the second sweep (> kOrthQ: list them again)
-    // one sample's flagged rows (bits eb over r, h, t, -, h', t') against w_r, in row order
-    auto fix_sample = [&](uint32_t eb, const int (&ids)[6]) {
-        const int er = ids[0];
-        if (er != wid) {  // w_r: kept in registers while consecutive samples share the relation
-            if (wid >= 0) {
+    int nq = 0;         // samples queued for the second sweep (> orth_q: list them again)
+    // A group of up to 64 samples (lane e: its rows' bits over r, h, t, -, h', t' and their
+    // ids), pair by pair in order: the next pair's row (and its w_r when the relation
+    // changes) is loaded while this pair's normOrth runs, so the wave waits for a load
+    // only when a pair re-reads the row just stored (then it keeps it in registers)
+    auto process_group = [&](int ng, uint32_t bits, const int (&eid)[6]) {
+        const uint32_t mb = l < ng ? bits & 0x37u : 0u;
+        const int cnt = __builtin_popcount(mb);
+        int pre = cnt;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const int v = __shfl_up(pre, d);
+            if (l >= d) pre += v;
+        }
+        {
+            int pos = pre - cnt;
+#pragma unroll
+            for (int q = 0; q < 6; ++q)
+                if ((mb >> q) & 1u) plist[pos++] = (l << 3) | q;
+        }
+        const int np = __shfl(pre, kWave - 1);
+        wave_lds_sync();
+        struct Pair {
+            int er, q, key;
+            T* row;
+        };
+        auto pair_at = [&](int p) {
+            const int info = __builtin_amdgcn_readfirstlane(plist[p]);
+            const int e = info >> 3, q = info & 7;
+            Pair P;
+            P.er = readlane_i32(eid[0], e);
+            const int id = q == 0 ? P.er : readlane_i32(q == 1 ? eid[1] : q == 2 ? eid[2] : q == 4 ? eid[4] : eid[5], e);
+            P.q = q;
+            // keys: relations [0, nr), w rows [nr, 2 nr), entities from 2 nr
+            P.key = q == 0 ? id : 2 * a.nr + id;
+            P.row = (q == 0 ? a.rel : a.ent) + (int64_t)id * a.ld;
+            return P;
+        };
+        if (np == 0) return;
+        Pair cur = pair_at(0);
+        RowReg<T, CH> A, An, Wn;
+        pend.before_load(cur.key);
+        row_load_sc1(A, cur.row, a.n);
+        for (int p = 0; p < np; ++p) {
+            if (cur.er != wid) {  // w_r: kept in registers while consecutive pairs share the relation
+                if (wid >= 0) {
+                    row_store_sc1(W, a.w + (int64_t)wid * a.ld, a.n);
+                    pend.add(a.nr + wid);
+                }
+                pend.before_load(a.nr + cur.er);
+                row_load_sc1(W, a.w + (int64_t)cur.er * a.ld, a.n);
+                wid = cur.er;
+            }
+            const bool more = p + 1 < np;
+            Pair nx{};
+            bool pre_a = false, pre_w = false;
+            if (more) {  // the next pair's rows in flight
+                nx = pair_at(p + 1);
+                pre_a = nx.key != cur.key;
+                if (pre_a) {
+                    pend.before_load(nx.key);
+                    row_load_sc1(An, nx.row, a.n);
+                }
+                pre_w = nx.er != cur.er;
+                if (pre_w) {
+                    pend.before_load(a.nr + nx.er);
+                    row_load_sc1(Wn, a.w + (int64_t)nx.er * a.ld, a.n);
+                }
+            }
+            work += (uint32_t)orth_norm<T, CH>(A, W, a.n, (T)a.lr);
+            row_store_sc1(A, cur.row, a.n);
+            pend.add(cur.key);
+            if (!more) break;
+            if (pre_a) A = An;  // (else the same row: A holds what was just stored)
+            if (pre_w) {
                 row_store_sc1(W, a.w + (int64_t)wid * a.ld, a.n);
                 pend.add(a.nr + wid);
+                W = Wn;
+                wid = nx.er;
             }
-            pend.before_load(a.nr + er);
-            row_load_sc1(W, a.w + (int64_t)er * a.ld, a.n);
-            wid = er;
+            cur = nx;
         }
-        for (int q = 0; q < 6; ++q) {
-            if (!((eb >> q) & 1u)) continue;
-            const bool isrel = q == 0 || q == 3;
-            T* row = (isrel ? a.rel : a.ent) + (int64_t)ids[q] * a.ld;
-            // ids: relations [0, nr), w rows [nr, 2 nr), entities from 2 nr
-            const int key = isrel ? ids[q] : 2 * a.nr + ids[q];
-            RowReg<T, CH> A;
-            pend.before_load(key);
-            row_load_sc1(A, row, a.n);
-            work += (uint32_t)orth_norm<T, CH>(A, W, a.n, (T)a.lr);
-            row_store_sc1(A, row, a.n);
-            pend.add(key);
-        }
+        wave_lds_sync();  // (plist is rebuilt by the next group)
     };
     // a sweep over the flag words, samples in order (sweep 1 only when the queue overflowed)
     auto sweep_flags = [&](int sweep) {
@@ -331,11 +390,11 @@ __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
             }
             wave_lds_sync();
             for (int g = 0; g < count; g += kWave) {
-                int k2 = -1, bits = 0;
+                int bits = 0;
                 int eid[6] = {0, 0, 0, 0, 0, 0};
                 uint32_t sh = 0;  // the entity rows several relations flagged (second sweep)
                 if (g + l < count) {  // this lane's list entry: ids from the sample stream
-                    k2 = list[g + l];
+                    const int k2 = list[g + l];
                     const int i0 = a.si[k2], j = a.sj[k2];
                     const bool sd = a.side[k2];
                     bits = a.orth_mask[k2];
@@ -364,15 +423,7 @@ __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
                     }
                     nq += __builtin_popcountll(qm);
                 }
-                const int ng = min(kWave, count - g);
-                for (int e = 0; e < ng; ++e) {
-                    const uint32_t eb = (uint32_t)readlane_i32(bits, e);
-                    if (eb == 0) continue;  // (the other sweep's pairs)
-                    const int er = readlane_i32(eid[0], e);
-                    const int ids[6] = {er, readlane_i32(eid[1], e), readlane_i32(eid[2], e), er,
-                                        readlane_i32(eid[4], e), readlane_i32(eid[5], e)};
-                    fix_sample(eb, ids);
-                }
+                process_group(min(kWave, count - g), (uint32_t)bits, eid);
             }
             wave_lds_sync();
         }
@@ -380,13 +431,18 @@ __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
     sweep_flags(0);
     if (nq <= a.orth_q) {
         wave_lds_sync();
-        for (int e = 0; e < nq; ++e) {
-            const int er = __builtin_amdgcn_readfirstlane(queue[1][e]);
-            const int ids[6] = {er, __builtin_amdgcn_readfirstlane(queue[2][e]),
-                                __builtin_amdgcn_readfirstlane(queue[3][e]), er,
-                                __builtin_amdgcn_readfirstlane(queue[4][e]),
-                                __builtin_amdgcn_readfirstlane(queue[5][e])};
-            fix_sample((uint32_t)__builtin_amdgcn_readfirstlane(queue[0][e]), ids);
+        for (int g = 0; g < nq; g += kWave) {  // the queue, 64 samples a group
+            uint32_t bits = 0;
+            int eid[6] = {0, 0, 0, 0, 0, 0};
+            if (g + l < nq) {
+                bits = (uint32_t)queue[0][g + l];
+                eid[0] = eid[3] = queue[1][g + l];
+                eid[1] = queue[2][g + l];
+                eid[2] = queue[3][g + l];
+                eid[4] = queue[4][g + l];
+                eid[5] = queue[5][g + l];
+            }
+            process_group(min(kWave, nq - g), bits, eid);
         }
     } else {
         sweep_flags(1);
