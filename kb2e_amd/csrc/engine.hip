@@ -108,7 +108,9 @@ struct kb2e_ctx {
     // made on the host, the rejection chain is resolved on the device.
     hipStream_t side_stream = nullptr;
     DevBuf words, levels, jfin, sidefin, filter_slots, filter_bloom, pr_dev, consumed_dev;
-    DevBuf trip;  // int4 per training triple: head, tail, relation, Bernoulli threshold (sample_len)
+    DevBuf trip;  // int4 per training triple: head, tail, relation, Bernoulli threshold (sample_len),
+                  // or packed in 8 bytes when the ids fit (trip_eb > 0; SamplerArgs::trip8)
+    int32_t trip_eb = 0, trip_rb = 0;
     DevBuf glibc_pow;  // M^(2^k) of the kGlibcBlock-word jump (glibc_starts_pow_kernel)
     DevBuf chain_table, chain_super, chain_sc, chain_ch, chain_overflow;  // the chain by chunks
     bool sampler_doubling = false;  // a sample longer than kChainEmax words was seen: pointer doubling
@@ -583,7 +585,10 @@ void launch_prefetch(kb2e_ctx* c) {
     SamplerArgs a{};
     a.words = c->words.as<int32_t>();
     a.nraw = nraw;
-    a.trip = c->trip.as<int4>();
+    a.trip = c->trip_eb ? nullptr : c->trip.as<int4>();
+    a.trip8 = c->trip_eb ? c->trip.as<uint64_t>() : nullptr;
+    a.eb = c->trip_eb;
+    a.rb = c->trip_rb;
     a.ntrain = (int32_t)c->ts.size();
     a.ne = c->cfg.num_entities;
     a.slots = c->filter_slots.as<uint64_t>();
@@ -1334,15 +1339,31 @@ kb2e_status kb2e_upload_triples(kb2e_ctx* c, const int32_t* h, const int32_t* t,
                 while (k < 1000 && (double)k < pr[q]) ++k;
                 thr[q] = k;
             }
-            std::vector<int32_t> tp((size_t)count * 4);
-            for (int64_t q = 0; q < count; ++q) {
-                tp[4 * q] = h[q];
-                tp[4 * q + 1] = t[q];
-                tp[4 * q + 2] = r[q];
-                tp[4 * q + 3] = thr[r[q]];
+            // 8 bytes a triple when two entity ids, a relation id and the threshold
+            // (< 1024) fit (FB15k 49 bits, K5 64); else 16 (KB2E_SAMPLER_TRIP16=1: tests)
+            const int eb = std::max(1, bits_for(std::max<int64_t>(c->cfg.num_entities - 1, 1)));
+            const int rb = std::max(1, bits_for(std::max<int64_t>(c->cfg.num_relations - 1, 1)));
+            const bool pack = 2 * eb + rb + 10 <= 64 && !getenv("KB2E_SAMPLER_TRIP16");
+            c->trip_eb = pack ? eb : 0;
+            c->trip_rb = pack ? rb : 0;
+            if (pack) {
+                std::vector<uint64_t> tp((size_t)count);
+                for (int64_t q = 0; q < count; ++q)
+                    tp[q] = (uint64_t)h[q] | (uint64_t)t[q] << eb | (uint64_t)r[q] << (2 * eb) |
+                            (uint64_t)thr[r[q]] << (2 * eb + rb);
+                c->trip.alloc(tp.size() * 8);
+                HIPCHK(hipMemcpy(c->trip.p, tp.data(), tp.size() * 8, hipMemcpyHostToDevice));
+            } else {
+                std::vector<int32_t> tp((size_t)count * 4);
+                for (int64_t q = 0; q < count; ++q) {
+                    tp[4 * q] = h[q];
+                    tp[4 * q + 1] = t[q];
+                    tp[4 * q + 2] = r[q];
+                    tp[4 * q + 3] = thr[r[q]];
+                }
+                c->trip.alloc(tp.size() * 4);
+                HIPCHK(hipMemcpy(c->trip.p, tp.data(), tp.size() * 4, hipMemcpyHostToDevice));
             }
-            c->trip.alloc(tp.size() * 4);
-            HIPCHK(hipMemcpy(c->trip.p, tp.data(), tp.size() * 4, hipMemcpyHostToDevice));
         }
         if (c->cfg.model != KB2E_TRANSE && c->parallel()) {
             // PARALLEL TransH/TransR: every relation is its own event row

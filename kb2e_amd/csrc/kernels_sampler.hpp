@@ -36,6 +36,8 @@ struct SamplerArgs {
     int64_t nraw;
     const int4* trip;       // per training triple: head, tail, relation, Bernoulli threshold
                             // (#k in [0,1000) with k < pr[r], pr = 1000*tailMean/(tailMean+headMean) or 500)
+    const uint64_t* trip8;  // the same packed in 8 bytes when it fits (null: trip): head | tail << eb |
+    int32_t eb, rb;         //   relation << 2 eb | threshold << (2 eb + rb); eb / rb bits of an entity / relation id
     int32_t ntrain, ne;
     const uint64_t* slots;  // filter hash table
     uint64_t mask;
@@ -101,9 +103,22 @@ __device__ __forceinline__ void sample_len_at(const SamplerArgs& a, int64_t p) {
     const int32_t* w = a.words;
     const int32_t i = dev_rand_max(w[p], w[p + 1], a.ntrain);
     int32_t j = dev_rand_max(w[p + 2], w[p + 3], a.ne);
-    const int4 tr = a.trip[i];  // one line for the triple and its threshold
-    const int32_t h = tr.x, t = tr.y, r = tr.z;
-    const bool tail = w[p + 4] % 1000 < tr.w;  // == (double)(rand() % 1000) < pr[r]
+    int32_t h, t, r, thr;  // one random read for the triple and its threshold
+    if (a.trip8) {  // (8 bytes: half the table, most of it in L2)
+        const uint64_t v = a.trip8[i];
+        const uint64_t em = (1ull << a.eb) - 1ull, rm = (1ull << a.rb) - 1ull;
+        h = (int32_t)(v & em);
+        t = (int32_t)((v >> a.eb) & em);
+        r = (int32_t)((v >> (2 * a.eb)) & rm);
+        thr = (int32_t)(v >> (2 * a.eb + a.rb));
+    } else {
+        const int4 tr = a.trip[i];
+        h = tr.x;
+        t = tr.y;
+        r = tr.z;
+        thr = tr.w;
+    }
+    const bool tail = w[p + 4] % 1000 < thr;  // == (double)(rand() % 1000) < pr[r]
     int64_t q = p + 5;
     uint8_t valid = 1;
     while (tail ? filter_has(a, h, r, j) : filter_has(a, j, r, t)) {

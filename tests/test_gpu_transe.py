@@ -156,11 +156,13 @@ def test_device_sampler_rejection_heavy(method):
     _oracle_vs_engine(ds, 16, 3, method=method, batches=7)
 
 
-@pytest.mark.parametrize("env", [("KB2E_SAMPLER_DOUBLING", "1"), ("KB2E_SAMPLER_EMAX", "7")])
+@pytest.mark.parametrize("env", [("KB2E_SAMPLER_DOUBLING", "1"), ("KB2E_SAMPLER_EMAX", "7"),
+                                 ("KB2E_SAMPLER_TRIP16", "1")])
 def test_device_sampler_chain_fallbacks(monkeypatch, env):
     """The pointer-doubling chain, forced, and reached through the chunked
     chain's overflow (entry offsets limited to 7 words: any sample with two
-    rejections at a chunk edge) draw the same reference stream."""
+    rejections at a chunk edge) draw the same reference stream; so does the
+    16-byte triple table sample_len reads when the ids do not fit 8 bytes."""
     monkeypatch.setenv(*env)
     _oracle_vs_engine(_dense_dataset(), 16, 3, method=1, batches=7)
 
