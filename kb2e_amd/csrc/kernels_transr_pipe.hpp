@@ -417,6 +417,8 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                     for (int s = 0; s < KS; ++s) reg[si * KS + s] = fma(ac[s], gc[si], reg[si * KS + s]);
                 }
         }
+        // the pair records: each helper its own slices' columns (the next chunk's
+        // projections overwrite the other slices' columns of this P buffer meanwhile)
 #pragma unroll
         for (int si = 0; si < NSW; ++si) {
             const int cb = hw + 3 * si;
