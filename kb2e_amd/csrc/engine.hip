@@ -154,6 +154,7 @@ struct kb2e_ctx {
     int32_t par_long_cap = 1, apply_grid = 256;
     DevBuf par_long_list, par_long_count;  // per epoch: long segments of every batch
     DevBuf hpar_orth;                      // PARALLEL TransH: orthogonality flags per sample
+    DevBuf hpar_ids;                       // ... and a flagged sample's ids [B][8]
     DevBuf hpar_tag;                       // PARALLEL TransH: per entity, the relations its flagged pairs have
     uint32_t hpar_stamp = 0;
     DevBuf hpar_count;                     // PARALLEL TransH: normOrth iterations of the last two batches
@@ -1149,6 +1150,7 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     if (g.model == KB2E_TRANSH && g.schedule == KB2E_SCHEDULE_PARALLEL) {
         c->hpar_orth.alloc((size_t)((c->B + 511) / 512) * 512);  // whole 8-byte words past B stay zero
         memset_sync(c->hpar_orth.p, 0, c->hpar_orth.bytes);
+        c->hpar_ids.alloc((size_t)c->B * 8 * 4);  // (written for the flagged samples before they are read)
         c->hpar_count.alloc(2 * 4);
         memset_sync(c->hpar_count.p, 0, c->hpar_count.bytes);
         const char* om = getenv("KB2E_HPAR_ORTH_MIN");  // tests: 0 always, a large value never

@@ -45,6 +45,7 @@ struct HParArgs {
     T* rel;
     T* w;
     uint8_t* orth_mask;       // [B] violating (update, row) pairs of each sample, bits u * 3 + {r, h, t}
+    int32_t* orth_ids;        // [B][8] a flagged sample's r, h, t, h', t' (check kernel; the one-wave pass)
     unsigned long long* ent_tag;  // [ne] stamp << 32 | multi << 31 | relation of the entity's flagged pairs
     uint32_t stamp;           // this batch's tag stamp (never 0)
     // normOrth's relation pass runs when the previous batch's normOrth work (its loop
@@ -98,17 +99,20 @@ __device__ __forceinline__ void transh_w_apply_body(HParArgs<T> a, int bid) {
     __syncthreads();
     T acc[CH][kVec] = {};
     bool act_any = false;
-    for (int base = p0 + w * kWave; base < p1; base += NWV * kWave) {
+    // the waves take G events at a time round-robin (one load round each), so the
+    // hottest relation's ~1,100 events spread over all NWV waves instead of whole
+    // 64-event chunks over the first few (30 -> ~19 us on FB15k-shaped batches)
+    constexpr int G = 16 / CH;
+    for (int base = p0 + w * G; base < p1; base += NWV * G) {
         const int p = base + l;
         int xrow = -1;
-        if (p < p1) {
+        if (l < G && p < p1) {
             const int32_t meta = a.meta[p];
             if (((meta & 3) - 1) != 0) xrow = meta >> 4;  // active update: kk * 2 + u
         }
         uint64_t m = __ballot(xrow >= 0);
         if (m) act_any = true;
         while (m) {  // G updates' delta rows (score kernel) in flight together, summed in event order
-            constexpr int G = 16 / CH;
             int ev[G], xr[G];
             int ne4 = 0;
             for (; ne4 < G && m; ++ne4) {
@@ -211,6 +215,10 @@ __global__ __launch_bounds__(256) void transh_orth_check_kernel(HParArgs<T> a) {
     }
     if (l == 0) {
         a.orth_mask[kk] = (uint8_t)mask;
+        if (mask) {  // the one-wave pass reads the ids here, one load level instead of three
+            *reinterpret_cast<int4*>(a.orth_ids + (int64_t)kk * 8) = make_int4(r, h, t, nh);
+            a.orth_ids[(int64_t)kk * 8 + 4] = nt;
+        }
         const int ids[6] = {r, h, t, r, nh, nt};
         for (int q = 1; q < 6; ++q)
             if (q != 3 && ((mask >> q) & 1u)) orth_tag_entity(a, ids[q], r);
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(256) void transh_orth_check_kernel(HParArgs<T> a) {
 // store.  w_r stays in registers while consecutive flagged samples share the
 // relation (the reference reloads what it just stored), and a store is drained
 // only before a later load of the same row (PendingRows).
-constexpr int kOrthWords = 4;  // 8-byte flag words per lane per pass
+constexpr int kOrthWords = 10;  // 8-byte flag words per lane per pass (5,120 samples: one pass on FB15k)
 // normOrth iterations of the previous batch from which normOrth takes the relation pass
 // (KB2E_HPAR_ORTH_MIN; a schedule choice only, the result is the same either way)
 constexpr uint32_t kOrthRelMin = 64;
@@ -366,7 +374,7 @@ __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
         for (int base = 0; base < a.B; base += 8 * kWave * kOrthWords) {
             uint64_t word[kOrthWords];
 #pragma unroll
-            for (int wi = 0; wi < kOrthWords; ++wi) {  // orth_mask is zero past B up to a multiple of 512
+            for (int wi = 0; wi < kOrthWords; ++wi) {  // (an 8-byte word at off < B: orth_mask is zero up to a multiple of 512)
                 const int off = base + 8 * (wi * kWave + l);
                 word[wi] = off < a.B ? *reinterpret_cast<const uint64_t*>(a.orth_mask + off) : 0ull;
             }
@@ -393,18 +401,16 @@ __global__ __launch_bounds__(64) void transh_orth_fix_kernel(HParArgs<T> a) {
                 int bits = 0;
                 int eid[6] = {0, 0, 0, 0, 0, 0};
                 uint32_t sh = 0;  // the entity rows several relations flagged (second sweep)
-                if (g + l < count) {  // this lane's list entry: ids from the sample stream
+                if (g + l < count) {  // this lane's list entry: ids as the check kernel left them
                     const int k2 = list[g + l];
-                    const int i0 = a.si[k2], j = a.sj[k2];
-                    const bool sd = a.side[k2];
+                    const int4 i4 = *reinterpret_cast<const int4*>(a.orth_ids + (int64_t)k2 * 8);
                     bits = a.orth_mask[k2];
-                    const int h = a.heads[i0], t = a.tails[i0], r = a.rels[i0];
-                    eid[0] = r;
-                    eid[1] = h;
-                    eid[2] = t;
-                    eid[3] = r;
-                    eid[4] = sd ? h : j;
-                    eid[5] = sd ? j : t;
+                    eid[0] = i4.x;
+                    eid[1] = i4.y;
+                    eid[2] = i4.z;
+                    eid[3] = i4.x;
+                    eid[4] = i4.w;
+                    eid[5] = a.orth_ids[(int64_t)k2 * 8 + 4];
 #pragma unroll
                     for (int q = 1; q < 6; ++q)
                         if (q != 3 && ((bits >> q) & 1) && orth_shared(a, eid[q])) sh |= 1u << q;
