@@ -82,28 +82,26 @@ __device__ __forceinline__ bool orth_shared(HParArgs<T> a, int e) {
     return (a.ent_tag[e] & 0x80000000ull) != 0;
 }
 
-// One NWV-wave workgroup per relation segment of the batch: waves sum chunks
-// of its events, partial sums combined in wave order, wave 0 applies.  The
-// hottest relation (~1100 events on FB15k-shaped batches) sets the time, so
-// the default is 16 waves (8 and 4 measured 16% and 50% slower).
+// One NWV-wave workgroup per NWV relation segments of the batch (most relations
+// have a few events: a 16-wave workgroup each was 1,345 workgroups a batch, bound
+// by dispatch, ~30 us).  A segment of at most kWSmall events is one wave's: its sum
+// in event order, the unit norm, the store.  The larger ones (the hot relations)
+// take the whole workgroup one after another: the waves take G events at a time
+// round-robin, partial sums combined in wave order, wave 0 applies.
+constexpr int kWSmall = 32;
+
 template <typename T, int CH, int NWV>
 __device__ __forceinline__ void transh_w_apply_body(HParArgs<T> a, int bid) {
     __shared__ T part[NWV][CH * kVec][kWave];
     __shared__ int any;
-    const int s = a.rel_begin[a.batch] + bid;
-    if (s >= a.batch_seg[a.batch + 1]) return;
+    const int sb = a.rel_begin[a.batch] + bid * NWV;
+    const int se = min(sb + NWV, a.batch_seg[a.batch + 1]);
+    if (sb >= se) return;
     const int w = threadIdx.x >> 6, l = lane_id();
-    const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
-    const int r = a.seg_row[s] - a.ne;
-    if (threadIdx.x == 0) any = 0;
-    __syncthreads();
-    T acc[CH][kVec] = {};
-    bool act_any = false;
-    // the waves take G events at a time round-robin (one load round each), so the
-    // hottest relation's ~1,100 events spread over all NWV waves instead of whole
-    // 64-event chunks over the first few (30 -> ~19 us on FB15k-shaped batches)
     constexpr int G = 16 / CH;
-    for (int base = p0 + w * G; base < p1; base += NWV * G) {
+    // the active events of [base, base + G) ∩ [p0, p1) (lanes < G) added to acc, their
+    // delta rows (score kernel) in flight together, summed in event order
+    auto add_events = [&](int base, int p1, T (&acc)[CH][kVec]) {
         const int p = base + l;
         int xrow = -1;
         if (l < G && p < p1) {
@@ -111,59 +109,91 @@ __device__ __forceinline__ void transh_w_apply_body(HParArgs<T> a, int bid) {
             if (((meta & 3) - 1) != 0) xrow = meta >> 4;  // active update: kk * 2 + u
         }
         uint64_t m = __ballot(xrow >= 0);
-        if (m) act_any = true;
-        while (m) {  // G updates' delta rows (score kernel) in flight together, summed in event order
-            int ev[G], xr[G];
-            int ne4 = 0;
-            for (; ne4 < G && m; ++ne4) {
-                ev[ne4] = __builtin_ctzll(m);
-                m &= m - 1;
-                xr[ne4] = readlane_i32(xrow, ev[ne4]);
-            }
-            T dv[G][CH][kVec];
+        const bool act = m != 0;
+        int ev[G], xr[G];
+        int ne4 = 0;
+        for (; ne4 < G && m; ++ne4) {
+            ev[ne4] = __builtin_ctzll(m);
+            m &= m - 1;
+            xr[ne4] = readlane_i32(xrow, ev[ne4]);
+        }
+        T dv[G][CH][kVec];
 #pragma unroll
-            for (int q = 0; q < G; ++q) {
-                if (q >= ne4) continue;
-                const T* drow = a.snap + (int64_t)xr[q] * a.ld;
+        for (int q = 0; q < G; ++q) {
+            if (q >= ne4) continue;
+            const T* drow = a.snap + (int64_t)xr[q] * a.ld;
 #pragma unroll
-                for (int cc = 0; cc < CH; ++cc)
+            for (int cc = 0; cc < CH; ++cc)
 #pragma unroll
-                    for (int k = 0; k < kVec; ++k) {
-                        const int el = cc * (kWave * kVec) + l * kVec + k;
-                        dv[q][cc][k] = el < a.n ? drow[el] : T(0);
-                    }
-            }
+                for (int k = 0; k < kVec; ++k) {
+                    const int el = cc * (kWave * kVec) + l * kVec + k;
+                    dv[q][cc][k] = el < a.n ? drow[el] : T(0);
+                }
+        }
 #pragma unroll
-            for (int q = 0; q < G; ++q) {
-                if (q >= ne4) continue;
+        for (int q = 0; q < G; ++q) {
+            if (q >= ne4) continue;
 #pragma unroll
-                for (int cc = 0; cc < CH; ++cc)
+            for (int cc = 0; cc < CH; ++cc)
 #pragma unroll
-                    for (int k = 0; k < kVec; ++k)
-                        if (elem_valid(cc, k, a.n)) acc[cc][k] += dv[q][cc][k];
+                for (int k = 0; k < kVec; ++k)
+                    if (elem_valid(cc, k, a.n)) acc[cc][k] += dv[q][cc][k];
+        }
+        return act;
+    };
+    // w_r += the sum, unit norm (a relation is touched only through an active update)
+    auto apply = [&](int s, const T (&sum)[CH][kVec]) {
+        const int r = a.seg_row[s] - a.ne;
+        RowReg<T, CH> W;
+        T* wrow = a.w + (int64_t)r * a.ld;
+        W.load(wrow, a.n);
+#pragma unroll
+        for (int cc = 0; cc < CH; ++cc)
+#pragma unroll
+            for (int k = 0; k < kVec; ++k)
+                if (elem_valid(cc, k, a.n)) W.v[cc][k] = W.v[cc][k] + sum[cc][k];
+        W.norm(a.n, false);
+        W.store(wrow, a.n);
+    };
+    {  // the small segments, a wave each
+        const int s = sb + w;
+        if (s < se) {
+            const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
+            if (p1 - p0 <= kWSmall) {
+                T acc[CH][kVec] = {};
+                bool act = false;
+                for (int base = p0; base < p1; base += G) act |= add_events(base, p1, acc);
+                if (act) apply(s, acc);
             }
         }
     }
+    for (int s = sb; s < se; ++s) {  // the large ones, all waves (uniform: every wave sees the sizes)
+        const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
+        if (p1 - p0 <= kWSmall) continue;
+        if (threadIdx.x == 0) any = 0;
+        __syncthreads();
+        T acc[CH][kVec] = {};
+        bool act = false;
+        for (int base = p0 + w * G; base < p1; base += NWV * G) act |= add_events(base, p1, acc);
 #pragma unroll
-    for (int cc = 0; cc < CH; ++cc)
+        for (int cc = 0; cc < CH; ++cc)
 #pragma unroll
-        for (int k = 0; k < kVec; ++k) part[w][cc * kVec + k][l] = acc[cc][k];
-    if (act_any && l == 0) atomicOr(&any, 1);
-    __syncthreads();
-    if (w != 0 || !any) return;
-    RowReg<T, CH> W;
-    T* wrow = a.w + (int64_t)r * a.ld;
-    W.load(wrow, a.n);
+            for (int k = 0; k < kVec; ++k) part[w][cc * kVec + k][l] = acc[cc][k];
+        if (act && l == 0) atomicOr(&any, 1);
+        __syncthreads();
+        if (w == 0 && any) {
+            T sum[CH][kVec];
 #pragma unroll
-    for (int cc = 0; cc < CH; ++cc)
+            for (int cc = 0; cc < CH; ++cc)
 #pragma unroll
-        for (int k = 0; k < kVec; ++k) {
-            T sum = part[0][cc * kVec + k][l];
-            for (int v = 1; v < NWV; ++v) sum += part[v][cc * kVec + k][l];
-            if (elem_valid(cc, k, a.n)) W.v[cc][k] = W.v[cc][k] + sum;
+                for (int k = 0; k < kVec; ++k) {
+                    sum[cc][k] = part[0][cc * kVec + k][l];
+                    for (int v = 1; v < NWV; ++v) sum[cc][k] += part[v][cc * kVec + k][l];
+                }
+            apply(s, sum);
         }
-    W.norm(a.n, false);
-    W.store(wrow, a.n);
+        __syncthreads();  // (part and any: the next large segment's)
+    }
 }
 
 template <typename T, int CH, int NWV>
@@ -172,7 +202,7 @@ __global__ __launch_bounds__(NWV * kWave) void transh_w_apply_kernel(HParArgs<T>
 }
 
 // Phase B's two sums in one launch (they touch disjoint tables): workgroups
-// [0, wgrid) the relation normals, the rest the TransE apply of the h/t/r rows,
+// [0, wgrid) the relation normals (16 segments each), the rest the TransE apply of the h/t/r rows,
 // so the hottest relation's normal overlaps the row sums instead of preceding them.
 template <typename T, int CH>
 __global__ __launch_bounds__(1024) void transh_phase_b_kernel(HParArgs<T> h, FoldArgs<T> fa, EventRecs er,

@@ -415,6 +415,16 @@ def test_transh_parallel_orth_requeue(orth_min, monkeypatch):
     _transh_vs_model(tiny(), 20, 2, orth_min=orth_min)
 
 
+@pytest.mark.parametrize("waves", [16, 4])
+def test_transh_parallel_unfused(waves, monkeypatch):
+    """KB2E_HPAR_FUSE=0: the relation normals and the row sums as two launches, the
+    normals' workgroups of 16 or 4 waves (as many relation segments each: the small
+    ones a wave's, the larger ones the whole workgroup's)."""
+    monkeypatch.setenv("KB2E_HPAR_FUSE", "0")
+    monkeypatch.setenv("KB2E_WAPPLY_WAVES", str(waves))
+    _transh_vs_model(data.synthetic("small", seed=1), 64, 1, batches=20, rate=0.001)
+
+
 def test_transh_parallel_small():
     _transh_vs_model(data.synthetic("small", seed=1), 64, 2, batches=20, rate=0.001)
 
