@@ -435,6 +435,21 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
     }
 
 
+def launch_ranks(n):
+    """Run this same command as `torch.distributed.run --nproc-per-node n` in a
+    child process (one rank per GPU, rendezvous on 127.0.0.1) and return its exit
+    code; rank 0's JSON line goes straight to this process's stdout."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.stdout.flush()
+    return subprocess.run(cmd).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -451,10 +466,18 @@ def main():
     ap.add_argument("--late-epoch", type=int, default=LATE_EPOCH,
                     help="also time the whole epoch with this index (steady state); 0: skip")
     args = ap.parse_args()
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus {args.gpus}: need at least one GPU")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` on its own: one rank per GPU, launched here as a child
+        # (nothing in this process has touched the GPU yet: numpy and kb2e_amd.data only)
+        sys.exit(launch_ranks(args.gpus))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the rank count must match the GPU count")
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -516,6 +539,11 @@ def main():
     }
     if main_run["merge"] is not None:
         out["merge"] = main_run["merge"]
+        ranks = main_run["merge"]["ranks"] or []
+        # the communicator's rank count as every rank saw it (min over ranks) and the
+        # device each rank drove: N distinct PCI buses = N GPUs
+        out["comm_nranks"] = min(r["comm_nranks"] for r in ranks) if ranks else None
+        out["pci_bus_ids"] = [r["pci_bus_id"] for r in ranks]
     out["schedules"] = {args.schedule: {"value": main_run["value"], "ms_per_step": main_run["ms_per_step"],
                                         "epoch": main_run["epoch"], "late_epoch": main_run["late_epoch"]}}
     if other_run is not None:

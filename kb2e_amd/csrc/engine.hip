@@ -1576,6 +1576,7 @@ kb2e_status kb2e_download_params(kb2e_ctx* c, double* e, double* r, double* w) {
     return guarded(c, [&] {
         HIPCHK(hipSetDevice(c->cfg.device));
         HIPCHK(hipStreamSynchronize(c->stream));
+        check_dataflow(c);  // tables a timed-out wait left are not handed out
         const int64_t ne = c->cfg.num_entities, nr = c->cfg.num_relations;
         if (c->f64()) {
             if (e) download_rows<double>(c, c->ent, e, ne, c->n, c->ld);
@@ -1657,6 +1658,7 @@ kb2e_status kb2e_synchronize(kb2e_ctx* c) {
         // the next epoch's sampling / index, queued on the side stream during
         // this one, is part of the work the caller waits for
         if (c->side_stream) HIPCHK(hipStreamSynchronize(c->side_stream));
+        check_dataflow(c);  // a bounded in-kernel wait that timed out fails here, not only in take_stats
         return KB2E_OK;
     });
 }

@@ -112,3 +112,59 @@ def test_merge_matches_numpy_renorm_of_summed_deltas(world):
         # each rank renormalised only its own entity block
         lo = min(NE, r * block)
         assert (0, lo, min(NE, lo + block) - lo) in calls
+
+
+# ---- bench.py's rank launch (the driver runs `bench.py --gpus N`) ----
+
+def _bench(args, env_extra):
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=120)
+
+
+def test_bench_refuses_a_rank_count_that_disagrees_with_gpus():
+    """--gpus 2 inside a 1-rank launch (and --gpus 1 inside a 2-rank one) exits
+    non-zero before any work: a scaling line must never be a 1-GPU line."""
+    out = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr, out.stderr[-500:]
+    out = _bench(["--steps", "1", "--warmup", "0"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert out.returncode != 0 and "WORLD_SIZE=2" in out.stderr, out.stderr[-500:]
+
+
+def test_bench_gpus_n_launches_n_ranks(monkeypatch):
+    """`bench.py --gpus 4` without WORLD_SIZE runs torch.distributed.run with four
+    ranks on 127.0.0.1 over this same command line, as a child process, and exits
+    with the child's code."""
+    import importlib
+    import subprocess
+    import sys
+
+    import bench
+
+    importlib.reload(bench)
+    seen = {}
+
+    class Done:
+        returncode = 7
+
+    def fake_run(cmd, *a, **k):
+        seen["cmd"] = cmd
+        return Done()
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 7
+    cmd = seen["cmd"]
+    i = cmd.index("torch.distributed.run")
+    assert cmd[i - 2] == sys.executable and cmd[i - 1] == "-m"
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "4" and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"] and cmd[-5].endswith("bench.py")

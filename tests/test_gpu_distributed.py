@@ -27,6 +27,26 @@ def test_bench_two_ranks_one_device(config):
     assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["config"]["parallelism"] == "dp2"
     assert d["value"] > 0 and d["config"]["global_batch"] == 2 * (d["config"]["global_batch"] // 2)
     assert 0.3 < d["active_fraction"] < 1.0
+    assert len(d["merge"]["ranks"]) == 2 and d["comm_nranks"] == 2 and len(d["pci_bus_ids"]) == 2
+
+
+@pytest.mark.gpu
+def test_bench_gpus_2_launches_its_own_ranks():
+    """The driver's form, `python3 bench.py --gpus 2` with no launcher around it:
+    bench.py starts torch.distributed.run itself (a child process, before any GPU
+    call) and the line is a 2-rank line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(KB2E_DIST_ONE_DEVICE="1", KB2E_DIST_BACKEND="gloo")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "60", "--warmup", "5",
+           "--config", "transe_fb15k", "--only", "--no-cpu-baseline", "--no-epoch"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert len(d["merge"]["ranks"]) == 2 and d["comm_nranks"] == 2
+    assert sorted(r["rank"] for r in d["merge"]["ranks"]) == [0, 1]
 
 
 def _merge_worker(rank, world, port, model, out):

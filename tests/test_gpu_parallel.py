@@ -428,3 +428,22 @@ def test_transh_parallel_unfused(waves, monkeypatch):
 def test_transh_parallel_small():
     _transh_vs_model(data.synthetic("small", seed=1), 64, 2, batches=20, rate=0.001)
 
+
+
+def test_transr_chain_wait_timeout_fails_loudly(monkeypatch):
+    """A bounded in-workgroup wait of the pipelined chain that times out (forced:
+    KB2E_CONS_DBG bit 32 keeps one helper wave from arriving) leaves invalid
+    tables; kb2e_synchronize and kb2e_download_params report it, not only
+    kb2e_take_stats (engine_relowner.inc check_dataflow)."""
+    monkeypatch.setenv("KB2E_CONS_DBG", "32")
+    ds = tiny()
+    eng = Engine("R", 20, ds.num_entities, ds.num_relations, rate=0.01, batches=20, seed=7, schedule="parallel")
+    eng.upload_triples(ds.train)
+    e0, r0, _ = eng.init_params()
+    eng.transr_seed(e0, r0)
+    eng.train_batches(1)
+    with pytest.raises(RuntimeError, match="timed out"):
+        eng.synchronize()
+    with pytest.raises(RuntimeError, match="timed out"):
+        eng.download_params()
+    eng.close()
