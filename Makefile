@@ -6,7 +6,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -Wall -Iinclude
 
-CSRC := $(filter-out kb2e_amd/csrc/eval.hip kb2e_amd/csrc/textio.hip kb2e_amd/csrc/transr_cons.hip kb2e_amd/csrc/kernels_transr_cons.hpp kb2e_amd/csrc/kernels_transr_wave.hpp kb2e_amd/csrc/kernels_transr_seq.hpp kb2e_amd/csrc/kernels_transr_pipe.hpp kb2e_amd/csrc/kernels_transr_chainw.hpp kb2e_amd/csrc/kernels_transr_chainwp.hpp kb2e_amd/csrc/kernels_transr_chainwv.hpp kb2e_amd/csrc/kernels_transr_chaing.hpp,$(wildcard kb2e_amd/csrc/*.hip kb2e_amd/csrc/*.hpp kb2e_amd/csrc/*.inc)) include/kb2e_engine.h
+CSRC := $(filter-out kb2e_amd/csrc/eval.hip kb2e_amd/csrc/textio.hip kb2e_amd/csrc/transr_cons.hip kb2e_amd/csrc/kernels_transr_cons.hpp kb2e_amd/csrc/kernels_transr_wave.hpp kb2e_amd/csrc/kernels_transr_seq.hpp kb2e_amd/csrc/kernels_transr_pipe.hpp kb2e_amd/csrc/kernels_transr_chainw.hpp kb2e_amd/csrc/kernels_transr_chainwp.hpp kb2e_amd/csrc/kernels_transr_chaing.hpp,$(wildcard kb2e_amd/csrc/*.hip kb2e_amd/csrc/*.hpp kb2e_amd/csrc/*.inc)) include/kb2e_engine.h
 
 BINS := bin/trainTransE bin/trainTransH bin/trainTransR bin/evalTransE bin/evalTransH bin/evalTransR
 
@@ -45,7 +45,7 @@ kb2e_amd/build/transr_cons.o: kb2e_amd/csrc/transr_cons.hip kb2e_amd/csrc/transr
 		kb2e_amd/csrc/kernels_transr_cons.hpp kb2e_amd/csrc/kernels_transr_wave.hpp kb2e_amd/csrc/kernels_transr_seq.hpp \
 		kb2e_amd/csrc/kernels_transr_pipe.hpp kb2e_amd/csrc/kernels_transr_mfma.hpp \
 		kb2e_amd/csrc/kernels_transr_chainw.hpp kb2e_amd/csrc/kernels_transr_chainwp.hpp \
-		kb2e_amd/csrc/kernels_transr_chainwv.hpp kb2e_amd/csrc/kernels_transr_chaing.hpp \
+		kb2e_amd/csrc/kernels_transr_chaing.hpp \
 		kb2e_amd/csrc/kernels_transr_parallel.hpp kb2e_amd/csrc/kernels_common.hpp kb2e_amd/csrc/hip_util.hpp
 	@mkdir -p kb2e_amd/build
 	$(HIPCC) $(HIPFLAGS) -c -o $@ kb2e_amd/csrc/transr_cons.hip

@@ -225,6 +225,14 @@ int32_t kb2e_rng_next(kb2e_ctx* ctx);
 kb2e_status kb2e_profile_enable(kb2e_ctx* ctx, int32_t on);
 kb2e_status kb2e_profile_query(kb2e_ctx* ctx, const char* name, double* total_ms, int64_t* launches);
 
+/* Schedule counters kept on the device (no reference counterpart: they say which
+ * branch of a schedule choice ran, for tests and tools).  Synchronises the
+ * context's stream.  Names: "transh_orth_rel_batches" -- PARALLEL TransH batches
+ * whose normOrth relation pass ran (the gate on the previous batch's normOrth
+ * work, kernels_transh_parallel.hpp); the other batches took the one-wave pass
+ * alone.  KB2E_EINVAL for an unknown name. */
+kb2e_status kb2e_counter(kb2e_ctx* ctx, const char* name, int64_t* value);
+
 /* Device memory footprint in bytes (tables + work buffers). */
 int64_t kb2e_device_bytes(const kb2e_ctx* ctx);
 

@@ -157,7 +157,7 @@ struct kb2e_ctx {
     DevBuf hpar_ids;                       // ... and a flagged sample's ids [B][8]
     DevBuf hpar_tag;                       // PARALLEL TransH: per entity, the relations its flagged pairs have
     uint32_t hpar_stamp = 0;
-    DevBuf hpar_count;                     // PARALLEL TransH: normOrth iterations of the last two batches
+    DevBuf hpar_count;                     // PARALLEL TransH: normOrth iterations of the last two batches, relation passes run
     uint32_t hpar_orth_min = 0;            // ... from which normOrth takes the relation pass
     int32_t hpar_orth_q = 0;               // the one-wave pass's second-sweep queue (kOrthQ)
     // PARALLEL schedule: per-event records in sorted order (kernels_transe.hpp EventRecs)
@@ -181,6 +181,12 @@ struct kb2e_ctx {
     DevBuf rpar_ptab;  // transRNorm pair dedupe: two per-batch (relation, entity) tables
     DevBuf rpar_batch_t0, rpar_td_r, rpar_td_cnt, rpar_td_kk, rpar_td_ent;  // per-epoch tile descriptors
     DevBuf sh_rpar_batch_t0, sh_rpar_td_r, sh_rpar_td_cnt, sh_rpar_td_kk, sh_rpar_td_ent;
+    // per batch: the relations it holds, most frequent first (the chain kernels' blocks), and
+    // their count, copied to pinned host memory with the index (the chain launches' grids)
+    DevBuf rpar_brel, sh_rpar_brel, rpar_bnrel, sh_rpar_bnrel;
+    int64_t rpar_brel_cap = 0;
+    int32_t* pin_bnrel = nullptr;
+    int32_t* pin_sh_bnrel = nullptr;
     hipStream_t fold_stream = nullptr;  // the long-segment fold runs beside the per-row fold
     hipEvent_t ev_fold_a = nullptr, ev_fold_b = nullptr;
     DevBuf long_list, long_count;
@@ -217,6 +223,8 @@ struct kb2e_ctx {
         if (pin_side) (void)hipHostFree(pin_side);
         if (pin_win) (void)hipHostFree(pin_win);
         if (pin_consumed) (void)hipHostFree(pin_consumed);
+        if (pin_bnrel) (void)hipHostFree(pin_bnrel);
+        if (pin_sh_bnrel) (void)hipHostFree(pin_sh_bnrel);
         flush_timers();
         if (ev_sampled) (void)hipEventDestroy(ev_sampled);
         if (ev_epoch_done) (void)hipEventDestroy(ev_epoch_done);
@@ -407,7 +415,8 @@ std::vector<std::pair<DevBuf*, DevBuf*>> index_bufs(kb2e_ctx* c) {
             {&c->rpar_tile_first, &c->sh_rpar_tile_first}, {&c->rpar_tiles, &c->sh_rpar_tiles},
             {&c->rpar_batch_t0, &c->sh_rpar_batch_t0}, {&c->rpar_td_r, &c->sh_rpar_td_r},
             {&c->rpar_td_cnt, &c->sh_rpar_td_cnt}, {&c->rpar_td_kk, &c->sh_rpar_td_kk},
-            {&c->rpar_td_ent, &c->sh_rpar_td_ent},
+            {&c->rpar_td_ent, &c->sh_rpar_td_ent}, {&c->rpar_brel, &c->sh_rpar_brel},
+            {&c->rpar_bnrel, &c->sh_rpar_bnrel},
 
             {&c->par_long_list, &c->sh_par_long_list}, {&c->par_long_count, &c->sh_par_long_count}};
 }
@@ -417,6 +426,7 @@ void swap_index(kb2e_ctx* c) {
         std::swap(pr.first->p, pr.second->p);
         std::swap(pr.first->bytes, pr.second->bytes);
     }
+    std::swap(c->pin_bnrel, c->pin_sh_bnrel);
 }
 
 void alloc_shadow_index(kb2e_ctx* c) {
@@ -1014,11 +1024,16 @@ void run_batches(kb2e_ctx* c, int64_t count) {
     for (int64_t q = 0; q < count; ++q) {
         if (c->epoch_pos == 0 && !c->epoch_ready) {
             start_epoch_stream(c);
+            // (PARALLEL TransR: the chain launches' grids, the batches' relation counts, come
+            // to the host with the index)
+            const bool counts = c->rpar_bnrel.p != nullptr;
             if (c->committed_gen >= 0 && c->index_pre_gen == c->committed_gen) {
                 HIPCHK(hipStreamWaitEvent(c->stream, c->ev_index, 0));  // built beside the previous epoch
+                if (counts) HIPCHK(hipEventSynchronize(c->ev_index));  // (long done: built an epoch ahead)
                 swap_index(c);
             } else {
                 build_index(c, c->stream, c->cur);
+                if (counts) HIPCHK(hipStreamSynchronize(c->stream));
             }
             c->epoch_ready = true;
             c->reduced_upto = 0;
@@ -1151,7 +1166,7 @@ void setup_epoch_buffers(kb2e_ctx* c) {
         c->hpar_orth.alloc((size_t)((c->B + 511) / 512) * 512);  // whole 8-byte words past B stay zero
         memset_sync(c->hpar_orth.p, 0, c->hpar_orth.bytes);
         c->hpar_ids.alloc((size_t)c->B * 8 * 4);  // (written for the flagged samples before they are read)
-        c->hpar_count.alloc(2 * 4);
+        c->hpar_count.alloc(3 * 4);  // (+ the batches whose relation pass ran: kb2e_counter)
         memset_sync(c->hpar_count.p, 0, c->hpar_count.bytes);
         const char* om = getenv("KB2E_HPAR_ORTH_MIN");  // tests: 0 always, a large value never
         c->hpar_orth_min = om ? (uint32_t)std::max(0, atoi(om)) : kOrthRelMin;
@@ -1836,6 +1851,20 @@ kb2e_status kb2e_profile_query(kb2e_ctx* c, const char* name, double* total_ms, 
         auto it = c->timers.find(name ? name : "");
         if (total_ms) *total_ms = it == c->timers.end() ? 0.0 : it->second.ms;
         if (launches) *launches = it == c->timers.end() ? 0 : it->second.launches;
+        return KB2E_OK;
+    });
+}
+
+kb2e_status kb2e_counter(kb2e_ctx* c, const char* name, int64_t* value) {
+    return guarded(c, [&] {
+        const std::string nm = name ? name : "";
+        if (nm != "transh_orth_rel_batches" || !value) return fail(c, KB2E_EINVAL, "unknown counter '" + nm + "'");
+        *value = 0;
+        if (!c->hpar_count.p) return KB2E_OK;  // (not a PARALLEL TransH context, or no triples yet)
+        uint32_t v = 0;
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipMemcpy(&v, (const uint32_t*)c->hpar_count.p + 2, 4, hipMemcpyDeviceToHost));
+        *value = v;
         return KB2E_OK;
     });
 }

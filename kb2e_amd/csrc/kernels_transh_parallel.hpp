@@ -55,6 +55,7 @@ struct HParArgs {
     uint32_t* orth_work_cur;    // this batch's iterations (relation and one-wave passes)
     uint32_t* orth_work_prev;   // the previous batch's (read by the relation pass, then zeroed)
     uint32_t orth_rel_min;
+    uint32_t* orth_rel_runs;    // batches whose relation pass ran (kb2e_counter "transh_orth_rel_batches")
     int32_t orth_q;             // second-sweep queue capacity (kOrthQ; KB2E_HPAR_ORTH_Q for the tests)
 };
 
@@ -501,6 +502,7 @@ template <typename T, int CH>
 __global__ __launch_bounds__(256) void transh_orth_rel_kernel(HParArgs<T> a) {
     // little normOrth work in the previous batch: leave every pair to the one-wave pass
     if (*a.orth_work_prev < a.orth_rel_min) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.orth_rel_runs, 1u);  // (kb2e_counter)
     const int s = a.rel_begin[a.batch] + (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
     if (s >= a.batch_seg[a.batch + 1]) return;
     const int l = lane_id();

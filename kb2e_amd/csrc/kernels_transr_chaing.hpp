@@ -48,7 +48,7 @@ template <typename T>
 __global__ __launch_bounds__(kGenThreads) void transr_cons_chain_gen_kernel(RParArgs a, RParBufs<T> bf) {
     constexpr int R = kGenRows, NT = kGenThreads, NW = NT / 64;
     // block b takes the b-th most frequent relation (the hot chains start first)
-    const int r = a.rel_order[blockIdx.x];
+    const int r = a.brel[blockIdx.x];
     int s;
     {
         int lo = a.rel_begin[a.batch], hi = a.batch_seg[a.batch + 1] - 1;

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(kWideThreads) void transr_cons_chain_wide_kernel(RP
     // relations start first (a hot relation dispatched late would add its wait to the
     // batch); its segment in this batch's index by binary search over the batch's
     // relation segments (sorted by row), none: nothing to do
-    const int r = a.rel_order[blockIdx.x];
+    const int r = a.brel[blockIdx.x];
     int s;
     {
         int lo = a.rel_begin[a.batch], hi = a.batch_seg[a.batch + 1] - 1;
@@ -705,54 +705,6 @@ static __attribute__((unused)) __global__ __launch_bounds__(kDaRelThreads) void 
     }
     __syncthreads();
     relation_records<kDaRelThreads>(a, bf, r, p0, ns, Wt, LT, gb, list, wsum);
-}
-
-// The pair records for n <= 128, a wave a record over the whole record array
-// (KB2E_RPAR_DA=wave; two elements a lane, G_i, i = 2l, 2l + 1; da_j = sum_i
-// W[j][i] G_i by interleaved wave sums, W from L2).
-static __attribute__((unused)) __global__ __launch_bounds__(256) void transr_cons_da_wide_kernel(RParArgs a,
-                                                                                                 RParBufs<double> bf) {
-    using T = double;
-    const int n = a.n, ld = a.ld, l = lane_id();
-    const int nrec = 4 * a.B + a.nr;
-    const int q = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    if (q >= nrec) return;
-    int r;
-    T* row;
-    bool ok;
-    if (q < 4 * a.B) {
-        const uint8_t ac = a.act[q >> 2], pf = bf.pflag[q];
-        const int i0 = a.si[q >> 2];
-        row = bf.pair + (int64_t)q * ld;
-        ok = ac && pf;
-        r = ok ? a.rels[i0] : 0;
-    } else {
-        r = q - 4 * a.B;
-        row = bf.relpair + (int64_t)r * ld;
-        ok = bf.relpair_stamp[r] == bf.stamp;
-    }
-    T g[2];
-    lane_pair_load(row, n, g);
-    if (!ok) return;
-    const T* W = bf.W + (int64_t)r * n * ld;
-    T da[2] = {T(0), T(0)};
-    for (int j0 = 0; j0 < n; j0 += 8) {
-        T v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            T wr[2] = {T(0), T(0)};
-            if (j0 + k < n) lane_pair_load(W + (int64_t)(j0 + k) * ld, n, wr);
-            v[k] = wr[0] * g[0] + wr[1] * g[1];
-        }
-        wave_sums<T, 8>(v);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (2 * l == j0 + k) da[0] = v[k];
-            if (2 * l + 1 == j0 + k) da[1] = v[k];
-        }
-    }
-    const T out[2] = {-(T)a.lr * da[0], -(T)a.lr * da[1]};
-    lane_pair_store(row, n, out);
 }
 
 }  // namespace kb2e

@@ -63,7 +63,7 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
     static_assert(NB <= NW - 1, "a column tile a helper wave");
     static_assert(2 * R * LA >= NB * NC, "the renorm's row partials borrow the P buffers");
     // block b takes the b-th most frequent relation (the hot chains start first)
-    const int r = a.rel_order[blockIdx.x];
+    const int r = a.brel[blockIdx.x];
     int s;
     {
         int lo = a.rel_begin[a.batch], hi = a.batch_seg[a.batch + 1] - 1;

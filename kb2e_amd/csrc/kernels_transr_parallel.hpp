@@ -75,8 +75,50 @@ struct RParArgs {
     const int32_t* td_cnt;    // [tiles] samples | 256 when the tile is its relation's only one
     const int32_t* td_kk;     // [tiles][8] batch-local sample of tile sample q
     const int32_t* td_ent;    // [tiles][8][4] entity of row (q, h / t / h' / t'), -1 past cnt
-    const int32_t* rel_order; // [nr] relation ids, most frequent in training first (chain kernels' block order)
+    const int32_t* brel;      // [nrel] this batch's relations, most frequent in training first (rel_list_kernel;
+                              // the chain kernels' block order: the long chains start first)
+    int32_t nrel;             // their count: the chain launches' grid
 };
+
+// Per batch b (a block each): the relations with a segment in the batch (segments
+// [rel_begin[b], batch_seg[b + 1]), sorted by row), listed in training-frequency order
+// (rel_order) -- the chain kernels' blocks, so that a launch covers exactly the
+// batch's relations, hot ones first -- and their count.
+static __attribute__((unused)) __global__ __launch_bounds__(1024) void rel_list_kernel(
+    const int32_t* rel_begin, const int32_t* batch_seg, const int32_t* seg_row, int32_t ne, const int32_t* rel_order,
+    int32_t nr, int64_t cap, int32_t* brel, int32_t* nrel) {
+    __shared__ int32_t wsum[16];
+    const int b = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int s0 = rel_begin[b], s1 = batch_seg[b + 1];
+    int32_t* out = brel + (int64_t)b * cap;
+    int total = 0;
+    for (int base = 0; base < nr; base += 1024) {
+        const int q = base + t;
+        const int r = q < nr ? rel_order[q] : -1;
+        bool here = false;
+        if (r >= 0 && s0 < s1) {
+            int lo = s0, hi = s1 - 1;
+            const int want = ne + r;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (seg_row[mid] < want) lo = mid + 1;
+                else hi = mid;
+            }
+            here = seg_row[lo] == want;
+        }
+        const uint64_t m = __ballot(here);
+        if (l == 0) wsum[w] = __popcll(m);
+        __syncthreads();
+        int off = total;
+        for (int k = 0; k < w; ++k) off += wsum[k];
+        int all = 0;
+        for (int k = 0; k < 16; ++k) all += wsum[k];
+        if (here) out[off + __popcll(m & ((1ull << l) - 1))] = r;
+        total += all;
+        __syncthreads();
+    }
+    if (t == 0) nrel[b] = total;
+}
 
 // The per-batch (relation, entity) -> first active update slot table.  A pair
 // (h', r), (t', r) or (entity[r], r) is the reference's repeated transRNorm

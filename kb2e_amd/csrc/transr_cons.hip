@@ -14,7 +14,6 @@
 #include "kernels_transr_seq.hpp"
 #include "kernels_transr_chainw.hpp"
 #include "kernels_transr_chainwp.hpp"
-#include "kernels_transr_chainwv.hpp"
 #include "kernels_transr_chaing.hpp"
 #include "kernels_transr_pipe.hpp"
 #include "kernels_transr_wave.hpp"
@@ -24,6 +23,9 @@ namespace kb2e {
 namespace {
 
 enum Kind { kCons, kGrad, kProj };
+
+// the chain kernels' grid: a workgroup per relation of the batch (a.brel)
+int chain_grid(const RParArgs& a) { return a.nrel > 0 ? a.nrel : 1; }
 
 template <typename T, int KS>
 const void* fn_at(Kind k) {
@@ -47,17 +49,6 @@ const void* kernel_fn(Kind k, int n) {
 template <typename T>
 const void* cons_fn(int n) {
     return kernel_fn<T>(kCons, n);
-}
-
-template <int... KS>
-const void* chain_table(int ks, std::integer_sequence<int, KS...>) {
-    const void* tab[] = {(const void*)transr_cons_chain_kernel<double, KS + 1>...};
-    return tab[ks - 1];
-}
-
-const void* chain_fn(int n) {
-    if (!cons_wave_supported(n)) throw std::runtime_error("transRNorm chain kernel: n > 64");
-    return chain_table((n + 3) / 4, std::make_integer_sequence<int, 16>{});
 }
 
 template <int... KS>
@@ -95,43 +86,18 @@ const void* chainwp_fn(int n) {
     throw std::runtime_error("transRNorm pipelined wide chain kernel: no instantiation");
 }
 
-const void* chainwv_fn(int n) {
-    switch (wp_ks(n)) {
-        case 18: return (const void*)transr_cons_chain_wv_kernel<18>;
-        case 20: return (const void*)transr_cons_chain_wv_kernel<20>;
-        case 22: return (const void*)transr_cons_chain_wv_kernel<22>;
-        case 24: return (const void*)transr_cons_chain_wv_kernel<24>;
-        case 25: return (const void*)transr_cons_chain_wv_kernel<25>;
-    }
-    throw std::runtime_error("transRNorm pipelined wide chain kernel (V on the helpers): no instantiation");
-}
-
 // 64 < n <= 100: the pipelined wide chain (kernels_transr_chainwp.hpp);
-// KB2E_RPAR_CHAIN=lockstep keeps the eight-wave lockstep kernel (A/B)
+// KB2E_RPAR_CHAIN=lockstep runs the eight-wave lockstep kernel there too (A/B)
 bool use_wpipe(int n) {
     const char* e = getenv("KB2E_RPAR_CHAIN");
-    return n > 64 && n <= kWPMaxN && !(e && (std::string(e) == "lockstep" || std::string(e) == "wide"));
-}
-// and KB2E_RPAR_CHAIN=wv its variant with V = p K0 made by the helper waves
-// (kernels_transr_chainwv.hpp)
-bool use_wv(int n) {
-    const char* e = getenv("KB2E_RPAR_CHAIN");
-    return use_wpipe(n) && e && std::string(e) == "wv";
-}
-
-// KB2E_RPAR_CHAIN=serial: the unpipelined chain kernel (kernels_transr_seq.hpp)
-bool use_pipe() {
-    const char* e = getenv("KB2E_RPAR_CHAIN");
-    return !(e && std::string(e) == "serial");
+    return n > 64 && n <= kWPMaxN && !(e && std::string(e) == "lockstep");
 }
 
 }  // namespace
 
 size_t cons_seq_setup(int n) {
-    const bool pipe = use_pipe();
-    const size_t lds = pipe ? pipe_lds<double>(n) : chain_lds<double>(n);
-    HIPCHK(hipFuncSetAttribute(pipe ? pipe_fn(n) : chain_fn(n), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)lds));
+    const size_t lds = pipe_lds<double>(n);
+    HIPCHK(hipFuncSetAttribute(pipe_fn(n), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     return lds;
 }
 
@@ -139,11 +105,9 @@ void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, size_t lds, 
     RParArgs aa = a;
     RParBufs<double> bb = bf;
     void* args[] = {&aa, &bb};
-    // (the LDS size was chosen by cons_seq_setup under the same switch)
-    // one workgroup per relation, most frequent first (chain_first_tile; those absent exit)
-    // (the pair records are made at the end of each relation's chain: chain_records)
-    HIPCHK(hipLaunchKernel(lds == pipe_lds<double>(a.n) && use_pipe() ? pipe_fn(a.n) : chain_fn(a.n), dim3(a.nr),
-                           dim3(kChainThreads), args, lds, stream));
+    // one workgroup per relation of the batch, most frequent first (chain_first_tile);
+    // the pair records are made at the end of each relation's chain (chain_records)
+    HIPCHK(hipLaunchKernel(pipe_fn(a.n), dim3(chain_grid(a)), dim3(kChainThreads), args, lds, stream));
 }
 
 bool cons_chainw_supported(int n) { return n >= 1 && n <= kWideMaxN; }
@@ -151,10 +115,10 @@ bool cons_chainw_supported(int n) { return n >= 1 && n <= kWideMaxN; }
 size_t cons_chainw_setup(int n) {
     HIPCHK(hipFuncSetAttribute((const void*)transr_cons_da_rel_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)da_rel_lds(n)));
-    const bool wp = use_wpipe(n), wv = use_wv(n);
-    const size_t lds = wv ? chainwv_lds(n) : wp ? chainwp_lds(n) : chainw_lds(n);
-    HIPCHK(hipFuncSetAttribute(wv ? chainwv_fn(n) : wp ? chainwp_fn(n) : chainw_fn(n),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const bool wp = use_wpipe(n);
+    const size_t lds = wp ? chainwp_lds(n) : chainw_lds(n);
+    HIPCHK(hipFuncSetAttribute(wp ? chainwp_fn(n) : chainw_fn(n), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
     return lds;
 }
 
@@ -164,22 +128,16 @@ void cons_chainw_launch(const RParArgs& a, const RParBufs<double>& bf, size_t ld
     RParArgs aa = a;
     RParBufs<double> bb = bf;
     void* args[] = {&aa, &bb};
-    // one workgroup per relation, most frequent first (those absent from the batch exit)
-    const int grid = a.nr;
+    // one workgroup per relation of the batch, most frequent first
+    const int grid = chain_grid(a);
     // (the LDS size was chosen by cons_chainw_setup under the same switch)
-    if (use_wv(a.n)) HIPCHK(hipLaunchKernel(chainwv_fn(a.n), dim3(grid), dim3(kWPThreads), args, lds, stream));
-    else if (use_wpipe(a.n)) HIPCHK(hipLaunchKernel(chainwp_fn(a.n), dim3(grid), dim3(kWPThreads), args, lds, stream));
-    else HIPCHK(hipLaunchKernel(chainw_fn(a.n), dim3(grid), dim3(kWideThreads), args, lds, stream));
-    // the pair records: a workgroup per relation, its final matrix staged once
-    // (KB2E_RPAR_DA=wave: a wave a record over the whole record array, W from L2; A/B)
-    const char* dv = getenv("KB2E_RPAR_DA");
     if (use_wpipe(a.n)) {
-        // (the pipelined chain makes its relation's records itself)
-    } else if (dv && std::string(dv) == "wave") {
-        const int da_grid = (int)(((int64_t)4 * a.B + a.nr + 3) / 4);  // a wave a record
-        HIPCHK(hipLaunchKernel((const void*)transr_cons_da_wide_kernel, dim3(da_grid), dim3(256), args, 0, stream));
+        // (the pipelined chain makes its relation's pair records itself)
+        HIPCHK(hipLaunchKernel(chainwp_fn(a.n), dim3(grid), dim3(kWPThreads), args, lds, stream));
     } else {
-        HIPCHK(hipLaunchKernel((const void*)transr_cons_da_rel_kernel, dim3(a.nr), dim3(kDaRelThreads), args,
+        HIPCHK(hipLaunchKernel(chainw_fn(a.n), dim3(grid), dim3(kWideThreads), args, lds, stream));
+        // the pair records: a workgroup per relation, its final matrix staged once
+        HIPCHK(hipLaunchKernel((const void*)transr_cons_da_rel_kernel, dim3(grid), dim3(kDaRelThreads), args,
                                da_rel_lds(a.n), stream));
     }
 }
@@ -233,9 +191,9 @@ void cons_chaing_launch(const RParArgs& a, const RParBufs<T>& bf, size_t lds, hi
     RParArgs aa = a;
     RParBufs<T> bb = bf;
     void* args[] = {&aa, &bb};
-    // one workgroup per relation, most frequent first (those absent from the batch exit)
-    HIPCHK(hipLaunchKernel((const void*)transr_cons_chain_gen_kernel<T>, dim3(a.nr), dim3(kGenThreads), args, lds,
-                           stream));
+    // one workgroup per relation of the batch, most frequent first
+    HIPCHK(hipLaunchKernel((const void*)transr_cons_chain_gen_kernel<T>, dim3(chain_grid(a)), dim3(kGenThreads), args,
+                           lds, stream));
 }
 template void cons_chaing_launch<double>(const RParArgs&, const RParBufs<double>&, size_t, hipStream_t);
 template void cons_chaing_launch<float>(const RParArgs&, const RParBufs<float>&, size_t, hipStream_t);

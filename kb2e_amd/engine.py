@@ -24,7 +24,7 @@ EXPORTS = [
     "kb2e_default_config", "kb2e_create", "kb2e_destroy", "kb2e_last_error", "kb2e_upload_triples",
     "kb2e_init_params", "kb2e_transr_seed", "kb2e_upload_params", "kb2e_download_params", "kb2e_get_transr_work",
     "kb2e_set_transr_work", "kb2e_set_sample_stream", "kb2e_get_sample_stream", "kb2e_train_epoch", "kb2e_train_batches",
-    "kb2e_synchronize", "kb2e_take_stats", "kb2e_rng_next", "kb2e_profile_enable", "kb2e_profile_query",
+    "kb2e_synchronize", "kb2e_take_stats", "kb2e_rng_next", "kb2e_profile_enable", "kb2e_profile_query", "kb2e_counter",
     "kb2e_device_bytes", "kb2e_device_tables", "kb2e_renormalize", "kb2e_evaluate", "kb2e_evaluate_transr_compat",
     "kb2e_renormalize_rows", "kb2e_init_params_device", "kb2e_write_table", "kb2e_format_table",
     "kb2e_read_table", "kb2e_comm_unique_id", "kb2e_comm_init_rank", "kb2e_comm_init_group", "kb2e_merge_epoch",
@@ -80,6 +80,7 @@ def lib():
             "kb2e_profile_enable": (i32, [vp, i32]),
             "kb2e_profile_query": (i32, [vp, C.c_char_p, dp, C.POINTER(i64)]),
             "kb2e_device_bytes": (i64, [vp]),
+            "kb2e_counter": (i32, [vp, C.c_char_p, C.POINTER(i64)]),
             "kb2e_device_tables": (i32, [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(i64),
                                          C.POINTER(i64), C.POINTER(i64)]),
             "kb2e_renormalize": (i32, [vp, u8p, u8p, u8p]),
@@ -293,6 +294,12 @@ class Engine:
         n = C.c_int64(0)
         self._check(lib().kb2e_profile_query(self.h, name.encode(), C.byref(ms), C.byref(n)), "profile_query")
         return ms.value, n.value
+
+    def counter(self, name):
+        """A device-side schedule counter (include/kb2e_engine.h kb2e_counter)."""
+        v = C.c_int64(0)
+        self._check(lib().kb2e_counter(self.h, name.encode(), C.byref(v)), "counter")
+        return v.value
 
     def renormalize(self, ent_rows=None, rel_rows=None, w_rows=None):
         keep = [None if m is None else np.ascontiguousarray(m, dtype=np.uint8) for m in (ent_rows, rel_rows, w_rows)]

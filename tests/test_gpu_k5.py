@@ -187,7 +187,7 @@ def test_k5_full_size_compat_energy(k5):
         eng.close()
 
 
-@pytest.mark.parametrize("chain", ["wv", "lockstep"])
+@pytest.mark.parametrize("chain", ["lockstep"])
 def test_k5_chain_kernels_agree(k5, chain, monkeypatch):
     """One full-size batch (compat energy) through each transRNorm chain kernel
     at n = 100 against the default one: the same pairs in the same order

@@ -85,7 +85,7 @@ def test_transe_parallel_deterministic():
 def _cons_form(dim, mfma):
     """The transRNorm form the engine runs (engine_transr_parallel.inc): the
     per-relation sequential chain (every pair against the matrix the earlier
-    ones left) in FP64 up to n = 112 -- kernels_transr_seq.hpp / _pipe.hpp on
+    ones left) in FP64 up to n = 112 -- kernels_transr_pipe.hpp on
     the n <= 64 matrix-core path, kernels_transr_chainwp.hpp at 64 < n <= 100,
     kernels_transr_chainw.hpp elsewhere -- unless
     KB2E_RPAR_CONS picks the Jacobi tile / wave kernels; Jacobi above 112."""
@@ -151,19 +151,18 @@ def test_transr_parallel_cons_tile_kernel(dim, distance, St, compat, monkeypatch
 @pytest.mark.parametrize("dim,St,compat", [(20, 8, False), (50, 4, True), (64, 2, True), (17, 8, False), (18, 8, False),
                                             (49, 8, False), (33, 4, True)])
 def test_transr_parallel_chain_widths(dim, St, compat, monkeypatch):
-    """The per-relation sequential transRNorm kernel (kernels_transr_seq.hpp) at
+    """The per-relation sequential transRNorm kernel (kernels_transr_pipe.hpp) at
     one to four column slices (n = 17 .. 64): relations of the tiny set hold ~90
     pairs a batch, so several 32-pair chunks and several violators a chunk, each
     pair against the matrix the earlier ones left."""
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=compat)
 
 
-@pytest.mark.parametrize("chain", ["pipe", "serial"])
 @pytest.mark.parametrize("dim,compat,env,St", [(50, True, "KB2E_RPAR_CHAIN_LIST=64", 8),
                                                (33, False, "KB2E_RPAR_CHAIN_LIST=64", 8),
                                                (50, True, "KB2E_RPAR_CHAIN_TILES=2", 1),
                                                (20, False, "KB2E_RPAR_CHAIN_TILES=3", 1)])
-def test_transr_parallel_chain_windows(dim, compat, env, St, chain, monkeypatch):
+def test_transr_parallel_chain_windows(dim, compat, env, St, monkeypatch):
     """The chain kernels over several windows of a relation's pairs
     (KB2E_RPAR_CHAIN_LIST=64 against ~90 pairs a relation a batch on the tiny
     set; FB15k's hottest relation fits one 1,536-pair window): W_c, K0 and the
@@ -174,12 +173,10 @@ def test_transr_parallel_chain_windows(dim, compat, env, St, chain, monkeypatch)
     W_c's rows are renormalised) must still be isolated there."""
     name, val = env.split("=")
     monkeypatch.setenv(name, val)
-    if chain == "serial":
-        monkeypatch.setenv("KB2E_RPAR_CHAIN", "serial")
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=compat)
 
 
-@pytest.mark.parametrize("chain", ["default", "lockstep", "wv"])
+@pytest.mark.parametrize("chain", ["default", "lockstep"])
 @pytest.mark.parametrize("dim,compat,mfma", [(100, True, False), (100, False, False), (72, True, True),
                                              (20, True, False), (88, False, True)])
 def test_transr_parallel_wide_chain_windows(dim, compat, mfma, chain, monkeypatch):
@@ -317,7 +314,7 @@ def test_transr_parallel_generic_chain_windows(monkeypatch):
 def test_transr_parallel_refuses_above_128(monkeypatch):
     """PARALLEL TransR trains n <= 128 (the VALU tile path holds two elements a
     lane); wider contexts are refused (KB2E_EUNSUPPORTED: the ORDERED schedule
-    trains up to 138)."""
+    trains every dim a context takes, up to 512)."""
     from kb2e_amd.engine import EngineError
     ds = tiny()
     with pytest.raises(EngineError, match="EUNSUPPORTED"):
@@ -347,7 +344,8 @@ def test_transr_parallel_fp32_chain_close(monkeypatch):
 
 def test_transr_parallel_fp32_close(monkeypatch):
     """FP32 tables: hinge decisions flip at the margin, so statistics, not elements.
-    (Both on the Jacobi transRNorm: the chunked chain is FP64 only.)"""
+    (Both on the Jacobi transRNorm, which KB2E_RPAR_CONS=jacobi asks for by name; by
+    default FP32 takes the generic pair-by-pair chain: test_transr_parallel_fp32_chain_close.)"""
     monkeypatch.setenv("KB2E_RPAR_CONS", "jacobi")
     ds = tiny()
     out = {}
