@@ -81,6 +81,14 @@ typedef struct {
                                transr/transr.cpp:20-25; 0: zeroed work vectors */
     int32_t device;         /* HIP device ordinal */
     int32_t schedule;       /* kb2e_schedule */
+    int32_t sub_batches;    /* PARALLEL TransR: each batch's summed updates, norms and
+                               transRNorm pairs applied in this many ordered sub-batches
+                               of ceil(B / k) samples (the energies, hinge decisions and
+                               update directions stay on the start-of-batch tables,
+                               common/trainer.cpp:132-133); nearer the reference's
+                               norm after every update (transr/trainer.cpp:174-187).
+                               1 = one per batch.  Ignored by the other models and the
+                               ORDERED schedule. */
 } kb2e_config;
 
 typedef struct kb2e_ctx kb2e_ctx;

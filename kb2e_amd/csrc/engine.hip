@@ -89,6 +89,11 @@ struct kb2e_ctx {
     int tables_read = 0;  // kb2e_read_table: bit t = table t loaded from text
     int n = 0, ld = 0, ch = 1, nw = 2, esize = 8;
     int64_t B = 0, nb = 0, S = 0;
+    // PARALLEL TransR sub-batches (kb2e_config.sub_batches): index batches a batch, their
+    // size (the last one the rest) and count (nbi = nb * sub; 1, B, nb otherwise)
+    int32_t sub = 1;
+    int64_t Bs = 0, nbi = 0;
+    DevBuf snap_ent, snap_rel, snap_w;  // the start-of-batch tables phase A reads (sub > 1)
     hipStream_t stream = nullptr;
     int64_t device_bytes = 0;
 
@@ -450,6 +455,8 @@ void build_index(kb2e_ctx* c, hipStream_t st, int set) {
     ka.owner = c->cfg.model == KB2E_TRANSE ? nullptr : c->owner.as<int32_t>();
     ka.nsamples = c->S;
     ka.B = (int32_t)c->B;
+    ka.sub = c->sub;
+    ka.Bs = (int32_t)c->Bs;
     ka.ne = c->cfg.num_entities;
     ka.kl = c->kl;
     ka.keys = c->keys.as<uint64_t>();
@@ -491,7 +498,7 @@ void build_index(kb2e_ctx* c, hipStream_t st, int set) {
                                                        c->nvalid.as<int32_t>());
         HIPCHK(hipGetLastError());
         batch_begin_kernel<<<256, 256, 0, st>>>(c->keys_sorted.as<uint64_t>(), c->seg_start.as<int32_t>(),
-                                                        c->nseg.as<int32_t>(), (int)c->nb, c->kl,
+                                                        c->nseg.as<int32_t>(), (int)c->nbi, c->kl,
                                                         c->batch_seg.as<int32_t>());
         HIPCHK(hipGetLastError());
         if (c->cfg.model != KB2E_TRANSE && !c->parallel()) build_owner_index(c);
@@ -1087,6 +1094,15 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     c->nb = g.num_batches;
     c->S = c->B * c->nb;
     if (c->B < 1) throw std::invalid_argument("fewer training triples than batches");
+    // PARALLEL TransR sub-batches: the event index cuts every batch into `sub` index
+    // batches of Bs samples (the last one the rest), each one phase B of its own
+    c->sub = 1;
+    c->Bs = c->B;
+    if (g.model == KB2E_TRANSR && g.schedule == KB2E_SCHEDULE_PARALLEL && g.sub_batches > 1) {
+        c->Bs = (c->B + g.sub_batches - 1) / g.sub_batches;
+        c->sub = (int32_t)((c->B + c->Bs - 1) / c->Bs);  // (the non-empty ones)
+    }
+    c->nbi = c->nb * c->sub;
     c->long_list.alloc((size_t)c->B * c->slots * 4);
     c->long_count.alloc(16);
     for (int q = 0; q < 2; ++q) {
@@ -1110,7 +1126,7 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     const int64_t nowners = g.model == KB2E_TRANSE ? g.num_relations : c->plan.num_owners;
     c->kl.kk_bits = bits_for(c->B);
     c->kl.row_bits = bits_for((int64_t)g.num_entities + nowners);
-    c->kl.batch_bits = bits_for(c->nb);  // holds nb, so batch nb-1 is never all-ones
+    c->kl.batch_bits = bits_for(c->nbi);  // holds nbi, so index batch nbi-1 is never all-ones
     if (c->kl.total_bits() > 64) throw std::invalid_argument("problem too large for 64-bit event keys");
     const int64_t nkeys = c->S * c->slots;
     if (nkeys >= (1ll << 31)) throw std::invalid_argument("epoch too large for one index (> 2^31 events)");
@@ -1121,7 +1137,7 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     c->seg_start.alloc((nkeys + 1) * 4);
     c->nseg.alloc(16);
     c->nvalid.alloc(16);
-    c->batch_seg.alloc((c->nb + 1) * 4);
+    c->batch_seg.alloc((c->nbi + 1) * 4);
     size_t t1 = 0, t2 = 0, t3 = 0;
     HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, t1, (uint64_t*)nullptr, (uint64_t*)nullptr, (int)nkeys, 0,
                                              c->kl.total_bits(), c->stream));
@@ -1259,6 +1275,7 @@ void kb2e_default_config(kb2e_config* cfg) {
     cfg->transr_compat = 1;
     cfg->device = 0;
     cfg->schedule = KB2E_SCHEDULE_ORDERED;
+    cfg->sub_batches = 1;
 }
 
 kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
@@ -1268,7 +1285,8 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
     if (g.model < 0 || g.model > 2 || g.dim < 1 || g.dim > 512 || g.num_entities < 1 || g.num_relations < 1 ||
         g.num_batches < 1 || (g.precision != 32 && g.precision != 64) || (g.method != 0 && g.method != 1) ||
         (g.distance != 0 && g.distance != 1) || (g.sampler != 0 && g.sampler != 1) ||
-        (g.schedule != KB2E_SCHEDULE_ORDERED && g.schedule != KB2E_SCHEDULE_PARALLEL))
+        (g.schedule != KB2E_SCHEDULE_ORDERED && g.schedule != KB2E_SCHEDULE_PARALLEL) || g.sub_batches < 1 ||
+        g.sub_batches > 64)
         return KB2E_EINVAL;
     if (g.model == KB2E_TRANSR && g.num_relations > g.num_entities) return KB2E_EINVAL;
     if (g.schedule == KB2E_SCHEDULE_PARALLEL && g.model == KB2E_TRANSR && g.dim > 128) return KB2E_EUNSUPPORTED;  // entityVec_next_[relation]

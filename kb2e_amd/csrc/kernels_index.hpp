@@ -26,6 +26,7 @@ struct KeyArgs {
     const int32_t* owner;  // relation -> owner (relation-owner schedules), else null
     int64_t nsamples;      // samples in the epoch buffer
     int32_t B;             // batch size
+    int32_t sub, Bs;       // index batches a batch, samples an index batch (the last one the rest; 1, B: one)
     int32_t ne;
     KeyLayout kl;
     uint64_t* keys;        // slots * nsamples
@@ -53,7 +54,9 @@ template <int SLOTS, bool ENTREL>
 __global__ __launch_bounds__(256) void emit_keys_kernel(KeyArgs a) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= a.nsamples) return;
-    const int b = (int)(k / a.B), kk = (int)(k % a.B);
+    // index batch (batch, sub-batch; kb2e_config.sub_batches) and the sample within it
+    const int q = (int)(k % a.B), sb = q / a.Bs;
+    const int b = (int)(k / a.B) * a.sub + sb, kk = q - sb * a.Bs;
     const int i = a.si[k], j = a.sj[k];
     const int h = a.heads[i], t = a.tails[i], r = a.rels[i];
     const int nh = a.side[k] ? h : j, nt = a.side[k] ? j : t;

@@ -434,7 +434,8 @@ __global__ __launch_bounds__(kWPThreads) void transr_cons_chain_wpipe_kernel(RPa
                 const T aa = readlane_f(dp, v);  // |a_v|^2
                 const T pV = s2[0], VV = s2[1];
                 const T pvd = pV + aa * pp, vvd = VV + T(2) * aa * pV + aa * aa * pp;
-                T rpp = __builtin_amdgcn_rcp(pp);  // v_rcp_f64 and one Newton step (as the pipe kernel)
+                T rpp = __builtin_amdgcn_rcp(pp);  // v_rcp_f64 and two Newton steps (as the pipe kernel)
+                rpp = fma(fma(-pp, rpp, T(1)), rpp, rpp);
                 rpp = fma(fma(-pp, rpp, T(1)), rpp, rpp);
                 const T kappa = pvd * rpp;
                 const T w2t = vvd - kappa * pvd;

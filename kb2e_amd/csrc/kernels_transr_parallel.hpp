@@ -1218,6 +1218,7 @@ struct RTileDescArgs {
     const int32_t* nseg;
     const int32_t* batch_seg;
     int32_t nb, St, ne, B;
+    int32_t sub, Bs;    // index batches a batch, samples an index batch (kb2e_config.sub_batches)
     KeyLayout kl;
     const int32_t* si;  // the epoch's sample stream
     const int32_t* sj;
@@ -1249,7 +1250,8 @@ static __attribute__((unused)) __global__ __launch_bounds__(256) void rtile_desc
         if (q < cnt) {
             const uint64_t key = a.keys[p0 + 2 * (f + q)];
             kk = a.kl.kk_of(key);
-            const int64_t k = (int64_t)a.kl.batch_of(key) * a.B + kk;
+            const int ib = a.kl.batch_of(key);
+            const int64_t k = (int64_t)(ib / a.sub) * a.B + (int64_t)(ib % a.sub) * a.Bs + kk;
             const int i0 = a.si[k], jj = a.sj[k];
             const int h = a.heads[i0], tt = a.tails[i0];
             const bool sd = a.side[k] != 0;

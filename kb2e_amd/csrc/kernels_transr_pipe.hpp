@@ -620,9 +620,13 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                         const T Vc = c < n ? (vv4[0] + vv4[1]) + (vv4[2] + vv4[3]) : T(0);
                         tick(7);
                         T s2[2] = {pv * Vc, Vc * Vc};
-                        // 1 / |p_v|^2: v_rcp_f64 and one Newton step (three dependent ops, not
-                        // the IEEE division's ten; kappa moves by an ulp or so)
+                        // 1 / |p_v|^2: v_rcp_f64 and two Newton steps, as LLVM's own f64 division
+                        // before its final correction (the reciprocal to within an ulp; kappa =
+                        // pvd / pp then differs from the quotient by at most an ulp or so, which
+                        // moves rho = 1 - 2 lr kappa by ~1e-3 ulp: no round test flips on it),
+                        // issued beside the wave sums, off the violator's critical path
                         T rpp = __builtin_amdgcn_rcp(pp);
+                        rpp = fma(fma(-pp, rpp, T(1)), rpp, rpp);
                         rpp = fma(fma(-pp, rpp, T(1)), rpp, rpp);
                         wave_sums<T, 2>(s2);
                         tick(8);

@@ -39,7 +39,7 @@ class Config(C.Structure):
         ("model", C.c_int32), ("dim", C.c_int32), ("num_entities", C.c_int32), ("num_relations", C.c_int32),
         ("learning_rate", C.c_double), ("margin", C.c_double), ("method", C.c_int32), ("distance", C.c_int32),
         ("num_batches", C.c_int32), ("seed", C.c_uint32), ("precision", C.c_int32), ("sampler", C.c_int32),
-        ("transr_compat", C.c_int32), ("device", C.c_int32), ("schedule", C.c_int32),
+        ("transr_compat", C.c_int32), ("device", C.c_int32), ("schedule", C.c_int32), ("sub_batches", C.c_int32),
     ]
 
 
@@ -120,7 +120,7 @@ class Engine:
 
     def __init__(self, model, dim, num_entities, num_relations, *, rate=0.001, margin=1.0, method=1,
                  distance=0, batches=100, seed=0, precision=64, sampler=SAMPLER_GLIBC, transr_compat=True,
-                 device=0, schedule="ordered"):
+                 device=0, schedule="ordered", sub_batches=None):
         self.kind = MODELS[model] if isinstance(model, str) else int(model)
         self.n, self.ne, self.nr = dim, num_entities, num_relations
         cfg = Config()
@@ -130,6 +130,8 @@ class Engine:
         cfg.num_batches, cfg.seed, cfg.precision, cfg.sampler = batches, seed, precision, sampler
         cfg.transr_compat, cfg.device = int(transr_compat), device
         cfg.schedule = SCHEDULES[schedule] if isinstance(schedule, str) else int(schedule)
+        if sub_batches is not None:  # (None: the engine's default, kb2e_default_config)
+            cfg.sub_batches = int(sub_batches)
         self.cfg = cfg
         h = C.c_void_p()
         st = lib().kb2e_create(C.byref(cfg), C.byref(h))

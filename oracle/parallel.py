@@ -74,8 +74,15 @@ def transe_parallel_batches(ent, rel, triples, si, sj, side, B, nbatches, *, rat
     return loss, active
 
 
+def sub_batch_bounds(B, sub):
+    """The sample ranges of a batch's `sub` sub-batches: ceil(B / sub) samples
+    each, the last one the rest (kb2e_config.sub_batches)."""
+    bs = -(-B // sub)
+    return [(j * bs, min(B, (j + 1) * bs)) for j in range(sub) if j * bs < B]
+
+
 def transr_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, rate, margin=1.0, l1=True,
-                            compat=False, work=None, St=32, constraint=True, cons="jacobi", stats=None):
+                            compat=False, work=None, St=32, constraint=True, cons="jacobi", stats=None, sub=1):
     """Train `nbatches` TransR batches of the PARALLEL schedule in place
     (kb2e_amd/csrc/kernels_transr_parallel.hpp).  Returns (loss, active).
 
@@ -86,6 +93,14 @@ def transr_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
     norms; then transRNorm (transr/trainer.cpp:35-64) on every (h', r), (t', r)
     pair of an active update and (entity'[r], r) once per relation, iterated
     while |W^T a|^2 > 1 (transr_constraint: `cons` picks the kernel's form).
+
+    sub > 1: the batch's phase B in `sub` ordered sub-batches (sub_batch_bounds):
+    the energies, hinge decisions and update directions (x, d = h - t, y = W x)
+    all come from the start-of-batch tables as before (the reference's snapshot,
+    common/trainer.cpp:132-133), and each sub-batch in turn sums its own deltas,
+    renormalises and runs its transRNorm pairs (first occurrences per relation per
+    sub-batch) -- nearer the reference's renormalisation after every update
+    (transr/trainer.cpp:174-187) by a factor `sub` in the samples summed per norm.
     """
     loss = 0.0
     active = 0
@@ -118,29 +133,33 @@ def transr_parallel_batches(ent, rel, W, triples, si, sj, side, B, nbatches, *, 
         dp, dn = (pt - ph) - R, (pnt - pnh) - R    # fresh projections (transr/trainer.cpp:147-157)
         xp = np.where(dp > 0, 1.0, -1.0) if l1 else 2.0 * dp
         xn = np.where(dn > 0, 1.0, -1.0) if l1 else 2.0 * dn
-        a = np.nonzero(act)[0]
-        ups = [(h[a], t[a], xp[a], rate), (nh[a], nt[a], xn[a], -rate)]  # c = -lr beta
-        dW = np.zeros_like(W)
-        dr = np.zeros_like(rel)
-        acc = np.zeros_like(ent)
         Wsnap = W.copy()
-        for (hh, tt, xx, c) in ups:
-            d = ent[hh] - ent[tt]
-            np.add.at(dW, r[a], c * np.einsum("kj,ki->kji", d, xx))
-            np.add.at(dr, r[a], c * xx)
-            y = np.einsum("kji,ki->kj", Wsnap[r[a]], xx)
-            np.add.at(acc, hh, c * y)
-            np.add.at(acc, tt, -c * y)
-        ra = np.unique(r[a])
-        W[ra] += dW[ra]
-        rel[ra] += dr[ra]
-        rel[ra] /= np.sqrt((rel[ra] ** 2).sum(1, keepdims=True))
-        W[ra] /= np.sqrt((W[ra] ** 2).sum(2, keepdims=True))
-        ea = np.unique(np.concatenate([h[a], t[a], nh[a], nt[a]]))
-        ent[ea] += acc[ea]
-        ent[ea] /= np.sqrt((ent[ea] ** 2).sum(1, keepdims=True))
-        if constraint:
-            transr_constraint(ent, W, h, t, nh, nt, r, act, rate, St, cons=cons, stats=stats)
+        d_pos, d_neg = ent[h] - ent[t], ent[nh] - ent[nt]  # the snapshot's h - t (phase A)
+        for (s0, s1) in sub_batch_bounds(B, sub):
+            in_sub = np.zeros(B, bool)
+            in_sub[s0:s1] = True
+            act_j = act & in_sub
+            a = np.nonzero(act_j)[0]
+            ups = [(h[a], t[a], xp[a], d_pos[a], rate), (nh[a], nt[a], xn[a], d_neg[a], -rate)]  # c = -lr beta
+            dW = np.zeros_like(W)
+            dr = np.zeros_like(rel)
+            acc = np.zeros_like(ent)
+            for (hh, tt, xx, d, c) in ups:
+                np.add.at(dW, r[a], c * np.einsum("kj,ki->kji", d, xx))
+                np.add.at(dr, r[a], c * xx)
+                y = np.einsum("kji,ki->kj", Wsnap[r[a]], xx)
+                np.add.at(acc, hh, c * y)
+                np.add.at(acc, tt, -c * y)
+            ra = np.unique(r[a])
+            W[ra] += dW[ra]
+            rel[ra] += dr[ra]
+            rel[ra] /= np.sqrt((rel[ra] ** 2).sum(1, keepdims=True))
+            W[ra] /= np.sqrt((W[ra] ** 2).sum(2, keepdims=True))
+            ea = np.unique(np.concatenate([h[a], t[a], nh[a], nt[a]]))
+            ent[ea] += acc[ea]
+            ent[ea] /= np.sqrt((ent[ea] ** 2).sum(1, keepdims=True))
+            if constraint:
+                transr_constraint(ent, W, h, t, nh, nt, r, act_j, rate, St, cons=cons, stats=stats)
     return loss, active
 
 

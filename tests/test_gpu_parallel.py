@@ -97,7 +97,7 @@ def _cons_form(dim, mfma):
 
 
 def _transr_vs_model(ds, dim, epochs, monkeypatch, *, St=8, compat=False, distance=0, batches=10, rate=0.01,
-                     seed=3, atol=1e-9, mfma=True):
+                     seed=3, atol=1e-9, mfma=True, sub=1):
     from oracle.parallel import transr_parallel_batches
     monkeypatch.setenv("KB2E_RPAR_ST", str(St))
     monkeypatch.setenv("KB2E_RPAR_MFMA", "1" if mfma else "0")
@@ -109,7 +109,7 @@ def _transr_vs_model(ds, dim, epochs, monkeypatch, *, St=8, compat=False, distan
     m.prep_train()
     pe, pr, pw = m.tables()
     eng = Engine("R", dim, ds.num_entities, ds.num_relations, rate=rate, distance=distance, batches=batches,
-                 seed=seed, schedule="parallel", transr_compat=compat)
+                 seed=seed, schedule="parallel", transr_compat=compat, sub_batches=sub)
     eng.upload_triples(ds.train)
     e0, r0, w0 = eng.init_params()
     assert np.array_equal(e0, pe) and np.array_equal(r0, pr) and np.array_equal(w0, pw)
@@ -120,7 +120,7 @@ def _transr_vs_model(ds, dim, epochs, monkeypatch, *, St=8, compat=False, distan
     for ep in range(epochs):
         si, sj, side = m.sample_stream(B * batches)
         lo, ao = transr_parallel_batches(pe, pr, pw, ds.train, si, sj, side, B, batches, rate=rate,
-                                         l1=distance == 0, compat=compat, work=work, St=St, cons=cons)
+                                         l1=distance == 0, compat=compat, work=work, St=St, cons=cons, sub=sub)
         lg, ag = eng.train_epoch()
         assert ag == ao, (ep, ag, ao)
         assert abs(lg - lo) <= 1e-9 * max(1.0, abs(lo))
@@ -445,3 +445,21 @@ def test_transr_chain_wait_timeout_fails_loudly(monkeypatch):
     with pytest.raises(RuntimeError, match="timed out"):
         eng.download_params()
     eng.close()
+
+
+@pytest.mark.parametrize("sub", [2, 3, 4])
+@pytest.mark.parametrize("dim,compat,mfma,St", [(50, True, True, 8), (20, False, True, 8), (33, True, False, 4),
+                                                 (100, True, False, 8), (100, False, True, 2)])
+def test_transr_parallel_sub_batches(dim, compat, mfma, St, sub, monkeypatch):
+    """kb2e_config.sub_batches: phase B of every batch in `sub` ordered
+    sub-batches of ceil(B / sub) samples (3 leaves a shorter last one), phase A on
+    the start-of-batch tables, against oracle/parallel.py with the same `sub`:
+    the pipelined chain (n = 50, 20), the lockstep / VALU paths (33), K5's width
+    on both phase-A paths (100)."""
+    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=compat, mfma=mfma, sub=sub)
+
+
+def test_transr_parallel_sub_batches_small_set(monkeypatch):
+    """Sub-batches on the 30k-triple set (a hot relation of ~700 samples a batch:
+    several chunks and windows a sub-batch), compat energy, n = 50."""
+    _transr_vs_model(data.synthetic("small", seed=1), 50, 1, monkeypatch, St=8, compat=True, rate=0.001, sub=4)

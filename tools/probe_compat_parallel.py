@@ -82,6 +82,8 @@ def main():
         print(f"ordered epoch {ep}: {ol[-1]} ({time.time() - t0:.0f} s)", file=sys.stderr)
     out["ordered"] = ol
     for v in args.variants.split(","):
+        # "<cons>/k<sub>": the form with phase B in `sub` ordered sub-batches
+        cons, sub = (v.split("/k")[0], int(v.split("/k")[1])) if "/k" in v else (v, 1)
         pe, pr, pw = ent.copy(), rel.copy(), W.copy()
         work = [np.zeros(dim), np.zeros(dim)]
         pl = []
@@ -90,7 +92,7 @@ def main():
             sl = slice(ep * S, (ep + 1) * S)
             st = {}
             loss, act = transr_parallel_batches(pe, pr, pw, ds.train, stream[0][sl], stream[1][sl], stream[2][sl], B,
-                                                NB, rate=0.001, compat=True, work=work, cons=v, stats=st)
+                                                NB, rate=0.001, compat=True, work=work, cons=cons, stats=st, sub=sub)
             pl.append({"loss": loss, "active": act, **st, **table_stats(pe, pr, pw, ds.train, rng)})
             print(f"parallel[{v}] epoch {ep}: {pl[-1]} ({time.time() - t0:.0f} s)", file=sys.stderr)
         out[f"parallel_{v}"] = pl
