@@ -247,7 +247,7 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
     batches = max(1, 100 // world)
     eng = Engine(model, dim, ds.num_entities, ds.num_relations, rate=rate, method=method, distance=distance,
                  batches=batches, seed=7 + rank, precision=args.precision, device=local if world > 1 else 0,
-                 schedule=schedule)
+                 schedule=schedule, sub_batches=args.sub_batches)
     eng.upload_triples(train)
     if shape == "k5":
         import numpy as np
@@ -358,6 +358,7 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
         dist.all_reduce(row, op=dist.ReduceOp.SUM)
         comm = [{"rank": int(x[1]), "comm_nranks": int(x[0]), "entity_block": [int(x[2]), int(x[3])],
                  "device": int(x[4]), "pci_bus_id": int(x[5])} for x in row.tolist()]
+    sub_batches = eng.cfg.sub_batches if model == "R" and schedule == "parallel" else 1
     eng.close()
     samples = steps * B
     if dist is not None:
@@ -420,6 +421,7 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
                      "share_of_timed": merge_s / elapsed, "kind": type(merger).__name__, "ranks": comm}
     return {
         "value": samples / elapsed, "ms_per_step": elapsed / steps * 1e3, "B": B, "batches": batches,
+        "sub_batches": sub_batches,
         "merge": merge_rec, "device_bytes_per_gpu": device_bytes,
         "epoch": epoch_rec,
         "late_epoch": late_rec,
@@ -460,6 +462,8 @@ def main():
     ap.add_argument("--schedule", default="parallel", choices=["ordered", "parallel"],
                     help="schedule of the headline value; the other one is reported beside it")
     ap.add_argument("--only", action="store_true", help="measure the --schedule only")
+    ap.add_argument("--sub-batches", type=int, default=None,
+                    help="PARALLEL TransR sub-batches (kb2e_config.sub_batches; default: the engine's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-epoch", action="store_true", help="skip the whole-epoch timing")
     ap.add_argument("--seed-epochs", type=int, default=SEED_EPOCHS)
@@ -530,7 +534,7 @@ def main():
                                f"per GPU, {args.schedule} schedule"
                                + (", compat energy, TransE-init" if model == "R" and shape != "k5" else ""),
                    "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "single",
-                   "schedule": args.schedule},
+                   "schedule": args.schedule, "sub_batches": main_run["sub_batches"]},
         "roofline": main_run["roofline"],
         "active_fraction": main_run["active_fraction"],
         "timing": "K batches from an epoch boundary (epoch sampling commit + index build inside"

@@ -94,6 +94,7 @@ struct kb2e_ctx {
     int32_t sub = 1;
     int64_t Bs = 0, nbi = 0;
     DevBuf snap_ent, snap_rel, snap_w;  // the start-of-batch tables phase A reads (sub > 1)
+    uint64_t wait_ticks = 0;            // relation-owner ticket waits: wall-clock bound (engine_relowner.inc)
     hipStream_t stream = nullptr;
     int64_t device_bytes = 0;
 

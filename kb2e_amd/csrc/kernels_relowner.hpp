@@ -103,12 +103,22 @@ __device__ __forceinline__ void row_store_sc1(const RowReg<T, CH>& R, T* row, in
     }
 }
 
-// Wait until done[e] == ticket (bounded; a timeout sets *err and gives up).
-__device__ __forceinline__ void wait_ticket(const uint32_t* done, int e, uint32_t ticket, uint32_t* err) {
+// Wait until done[e] == ticket (bounded; a timeout sets *err and gives up).  The
+// bound is wall-clock time (wall_clock64 ticks, OwnerArgs::wait_ticks): a wait
+// lasts at most as long as the dependency chain in front of it, which at wide
+// dims is seconds (ORDERED TransR at dim 512 on the L2-resident matrix), so a
+// spin count would time out on a healthy batch.
+__device__ __forceinline__ bool wait_expired(uint32_t& spins, long long t0, uint64_t ticks) {
+    return (++spins & 255u) == 0 && (uint64_t)(wall_clock64() - t0) > ticks;
+}
+
+__device__ __forceinline__ void wait_ticket(const uint32_t* done, int e, uint32_t ticket, uint32_t* err,
+                                            uint64_t ticks) {
     uint32_t spins = 0;
+    const long long t0 = wall_clock64();
     while (__hip_atomic_load((gu32*)(done + e), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ticket) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 26)) {
+        if (wait_expired(spins, t0, ticks)) {
             __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
@@ -379,6 +389,7 @@ struct OwnerArgs {
     const uint32_t* tickets;
     uint32_t* done;
     uint32_t* err;
+    uint64_t wait_ticks;  // a ticket wait gives up after this many wall_clock64 ticks (the host: 600 s)
     T* ent;
     T* rel;
     T* w;        // TransH normals (live) / TransR matrices: next (W_B)
@@ -514,8 +525,9 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin
 
 // Wait until done[e_q] == tick_q for every slot (polls issued together).
 __device__ __forceinline__ void wait_tickets3(const uint32_t* done, int count, const uint32_t* e, const uint32_t* tk,
-                                              uint32_t* err) {
+                                              uint32_t* err, uint64_t ticks) {
     uint32_t spins = 0;
+    const long long t0 = wall_clock64();
     for (;;) {
         const uint32_t f0 = __hip_atomic_load((gu32*)(done + e[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t f1 = count > 1 ? __hip_atomic_load((gu32*)(done + e[1]), __ATOMIC_RELAXED,
@@ -524,7 +536,7 @@ __device__ __forceinline__ void wait_tickets3(const uint32_t* done, int count, c
                                                           __HIP_MEMORY_SCOPE_AGENT) : tk[2];
         if (f0 == tk[0] && f1 == tk[1] && f2 == tk[2]) return;
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 26)) {
+        if (wait_expired(spins, t0, ticks)) {
             __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
@@ -662,7 +674,7 @@ __global__ __launch_bounds__(64) void transh_owner_kernel(OwnerArgs<T> a, const 
         }
         if (it + 1 < m) nin.load(a, n0, n);
         OWNER_MARK(0);
-        wait_tickets3(a.done, count, ent, tk, a.err);
+        wait_tickets3(a.done, count, ent, tk, a.err, a.wait_ticks);
         OWNER_MARK(1);
         RowReg<T, CH> E0, E1;
         row_load_sc1(E0, a.ent + (int64_t)ent[0] * a.ld, n);
@@ -1074,7 +1086,7 @@ __global__ __launch_bounds__(64) void transr_owner_kernel(OwnerArgs<T> a, uint32
             __syncthreads();
         }
         OWNER_MARK(0);
-        for (int q = 0; q < d.count; ++q) wait_ticket(a.done, d.ent[q], d.tick[q], a.err);
+        for (int q = 0; q < d.count; ++q) wait_ticket(a.done, d.ent[q], d.tick[q], a.err, a.wait_ticks);
         OWNER_MARK(1);
         // slots: head is slot 0; tail/entrel slots by identity
         int tslot = 0, eslot = 0;
@@ -1397,7 +1409,7 @@ __global__ __launch_bounds__(64) void transr_owner_reg_kernel(OwnerArgs<T> a, co
         dirty = true;
         OWNER_MARK(3);
         // ---- entity rows
-        wait_tickets3(a.done, count, ent, tk, a.err);
+        wait_tickets3(a.done, count, ent, tk, a.err, a.wait_ticks);
         OWNER_MARK(1);
         T v0 = row_lane ? load_sc1(a.ent + (int64_t)ent[0] * ld + l) : T(0);
         T v1 = (count > 1 && row_lane) ? load_sc1(a.ent + (int64_t)ent[1] * ld + l) : T(0);

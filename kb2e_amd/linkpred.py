@@ -48,13 +48,15 @@ def transe_seed(ds, dim, epochs, *, rate=0.001, seed=7, batches=100, device=0):
 
 
 def train_and_evaluate(ds, model, dim, schedule, epochs, *, test=None, rate=0.001, method=1, distance=0,
-                       batches=100, seed=7, transr_compat=True, seed_tables=None, device=0, log=None):
+                       batches=100, seed=7, transr_compat=True, seed_tables=None, device=0, log=None,
+                       sub_batches=None):
     """Train `epochs` epochs with one schedule and evaluate; returns a dict with
     the four EmbeddingEvaluation::run numbers, losses and timing."""
     test = ds.test if test is None else test
     filt = np.concatenate([ds.train, ds.valid, ds.test])
     eng = Engine(model, dim, ds.num_entities, ds.num_relations, rate=rate, method=method, distance=distance,
-                 batches=batches, seed=seed, transr_compat=transr_compat, device=device, schedule=schedule)
+                 batches=batches, seed=seed, transr_compat=transr_compat, device=device, schedule=schedule,
+                 sub_batches=sub_batches)
     try:
         eng.upload_triples(ds.train)
         ent, rel, _ = eng.init_params()

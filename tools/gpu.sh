@@ -8,7 +8,7 @@
 #   bash tools/gpu.sh bench    <tag> [bench.py args]        one bench line (default: the driver's)
 #   bash tools/gpu.sh ab       <tag> <config> <VAR> <v1> [v2 ...]   100-batch lines per env setting ("-" = unset)
 #   bash tools/gpu.sh profile  <tag> <schedule> [bench args]  bench + rocprofv3 trace + HBM / f64-MFMA PMC passes
-#   bash tools/gpu.sh envelope <tag> <model> <dim> <compat> <epochs> <seeds> [batches] [schedules]
+#   bash tools/gpu.sh envelope <tag> <model> <dim> <compat> <epochs> <seeds> [batches] [schedules] [sub-batches]
 #   bash tools/gpu.sh hits     <tag>                        FB15k-shaped Hits@10 schedule parity, four configs
 #   bash tools/gpu.sh k5       <tag>                        n > 64 parity tests, K5 tests, the K5 line
 #   bash tools/gpu.sh final    <tag>                        suite + default line + K5 line
@@ -88,9 +88,9 @@ PY
         python3 bench.py $PASS "$@" > "$OUT/pmc_MFMA.log" 2>&1 || fail "pmc MFMA" $? "$OUT/pmc_MFMA.log"
     echo profile done ;;
   envelope)
-    MODEL=$1; DIM=$2; COMPAT=$3; EP=$4; SEEDS=$5; NB=${6:-100}; SCH=${7:-ordered,parallel}
+    MODEL=$1; DIM=$2; COMPAT=$3; EP=$4; SEEDS=$5; NB=${6:-100}; SCH=${7:-ordered,parallel}; SUB=${8:-}
     timeout -k 10 1150 python -u tools/seed_envelope.py --model "$MODEL" --dim "$DIM" --compat "$COMPAT" --epochs "$EP" \
-        --seed-epochs 500 --seeds "$SEEDS" --batches "$NB" --schedules "$SCH" --out "$OUT/envelope.jsonl" \
+        --seed-epochs 500 --seeds "$SEEDS" --batches "$NB" --schedules "$SCH" ${SUB:+--sub $SUB} --out "$OUT/envelope.jsonl" \
         > "$OUT/envelope.log" 2>&1 || fail envelope $? "$OUT/envelope.log"
     grep "^seed" "$OUT/envelope.log" ;;
   hits)

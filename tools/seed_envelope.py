@@ -94,6 +94,7 @@ def main():
     ap.add_argument("--batches", type=int, default=100, help="batches an epoch (the reference's --batches)")
     ap.add_argument("--seeds", default="7,8,9")
     ap.add_argument("--schedules", default="ordered,parallel")
+    ap.add_argument("--sub", type=int, default=None, help="PARALLEL TransR sub-batches (kb2e_config.sub_batches)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--summarize", nargs="*", default=None,
                     help="only write the summary of the per-seed rows in these JSONL files (runs split over calls)")
@@ -132,7 +133,10 @@ def main():
                "seed_epochs": args.seed_epochs, "transr_compat": bool(args.compat), "test": int(len(test))}
         for s in schedules:
             r = train_and_evaluate(ds, args.model, dim, s, args.epochs, test=test, seed=seed, batches=args.batches,
-                                   transr_compat=bool(args.compat), seed_tables=seed_tables, log=log)
+                                   transr_compat=bool(args.compat), seed_tables=seed_tables, log=log,
+                                   sub_batches=args.sub if s == "parallel" else None)
+            if s == "parallel" and args.sub is not None:
+                r["sub_batches"] = args.sub
             ls = [x[1] for x in r["losses"]]
             r["final_loss"] = ls[-1]
             r["mean_loss_last10"] = float(np.mean(ls[-10:]))
