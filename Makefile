@@ -6,7 +6,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -Wall -Iinclude
 
-CSRC := $(filter-out kb2e_amd/csrc/eval.hip kb2e_amd/csrc/textio.hip kb2e_amd/csrc/transr_cons.hip kb2e_amd/csrc/kernels_transr_cons.hpp kb2e_amd/csrc/kernels_transr_wave.hpp kb2e_amd/csrc/kernels_transr_seq.hpp kb2e_amd/csrc/kernels_transr_pipe.hpp kb2e_amd/csrc/kernels_transr_chainw.hpp kb2e_amd/csrc/kernels_transr_chainwp.hpp kb2e_amd/csrc/kernels_transr_chaing.hpp,$(wildcard kb2e_amd/csrc/*.hip kb2e_amd/csrc/*.hpp kb2e_amd/csrc/*.inc)) include/kb2e_engine.h
+CSRC := $(filter-out kb2e_amd/csrc/eval.hip kb2e_amd/csrc/textio.hip kb2e_amd/csrc/transr_cons.hip kb2e_amd/csrc/kernels_transr_cons.hpp kb2e_amd/csrc/kernels_transr_wave.hpp kb2e_amd/csrc/kernels_transr_seq.hpp kb2e_amd/csrc/kernels_transr_pipe.hpp kb2e_amd/csrc/kernels_transr_chainw.hpp kb2e_amd/csrc/kernels_transr_chainwp.hpp kb2e_amd/csrc/kernels_transr_chaing.hpp kb2e_amd/csrc/transr_wide.hip kb2e_amd/csrc/kernels_transr_widep.hpp,$(wildcard kb2e_amd/csrc/*.hip kb2e_amd/csrc/*.hpp kb2e_amd/csrc/*.inc)) include/kb2e_engine.h
 
 BINS := bin/trainTransE bin/trainTransH bin/trainTransR bin/evalTransE bin/evalTransH bin/evalTransR
 
@@ -50,7 +50,14 @@ kb2e_amd/build/transr_cons.o: kb2e_amd/csrc/transr_cons.hip kb2e_amd/csrc/transr
 	@mkdir -p kb2e_amd/build
 	$(HIPCC) $(HIPFLAGS) -c -o $@ kb2e_amd/csrc/transr_cons.hip
 
-kb2e_amd/libkb2e.so: kb2e_amd/build/engine.o kb2e_amd/build/eval.o kb2e_amd/build/textio.o kb2e_amd/build/transr_cons.o
+kb2e_amd/build/transr_wide.o: kb2e_amd/csrc/transr_wide.hip kb2e_amd/csrc/transr_cons.hpp \
+		kb2e_amd/csrc/kernels_transr_widep.hpp kb2e_amd/csrc/kernels_transr_seq.hpp kb2e_amd/csrc/kernels_transr_mfma.hpp \
+		kb2e_amd/csrc/kernels_transr_parallel.hpp kb2e_amd/csrc/kernels_common.hpp kb2e_amd/csrc/hip_util.hpp
+	@mkdir -p kb2e_amd/build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ kb2e_amd/csrc/transr_wide.hip
+
+kb2e_amd/libkb2e.so: kb2e_amd/build/engine.o kb2e_amd/build/eval.o kb2e_amd/build/textio.o kb2e_amd/build/transr_cons.o \
+		kb2e_amd/build/transr_wide.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 # diagnostic build: per-phase cycle counters in the relation-owner kernels
@@ -61,7 +68,7 @@ kb2e_amd/build/engine_prof.o: $(CSRC)
 	$(HIPCC) $(HIPFLAGS) -DKB2E_OWNER_PROF -c -o $@ kb2e_amd/csrc/engine.hip
 
 kb2e_amd/libkb2e_prof.so: kb2e_amd/build/engine_prof.o kb2e_amd/build/eval.o kb2e_amd/build/textio.o \
-		kb2e_amd/build/transr_cons.o
+		kb2e_amd/build/transr_cons.o kb2e_amd/build/transr_wide.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 oracle:
@@ -116,7 +123,8 @@ $(SANOBJ)/%.o: kb2e_amd/csrc/%.hip $(CSRC)
 	@mkdir -p $(SANOBJ)
 	$(HIPCC) $(HIPFLAGS) $(HIPSAN) -g -c -o $@ $<
 
-kb2e_amd/libkb2e_san.so: $(SANOBJ)/engine.o $(SANOBJ)/eval.o $(SANOBJ)/textio.o $(SANOBJ)/transr_cons.o
+kb2e_amd/libkb2e_san.so: $(SANOBJ)/engine.o $(SANOBJ)/eval.o $(SANOBJ)/textio.o $(SANOBJ)/transr_cons.o \
+		$(SANOBJ)/transr_wide.o
 	$(HIPCC) $(HIPFLAGS) $(HIPSAN) -shared-libasan -shared -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 bin/san/kb2e: kb2e_amd/csrc/host/kb2e_cli.cpp include/kb2e_engine.h kb2e_amd/libkb2e_san.so

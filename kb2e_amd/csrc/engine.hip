@@ -94,6 +94,11 @@ struct kb2e_ctx {
     int32_t sub = 1;
     int64_t Bs = 0, nbi = 0;
     DevBuf snap_ent, snap_rel, snap_w;  // the start-of-batch tables phase A reads (sub > 1)
+    // sub > 1: the second set of phase A's exports (phase A of sub-batch j + 1 runs on
+    // suba_stream beside phase B of sub-batch j) and the events that order them
+    DevBuf sb_x, sb_d, sb_y, sb_wpart, sb_rpart, sb_pflag, sb_cons_tile, sb_cpairs, sb_vio, sb_cnrows;
+    hipStream_t suba_stream = nullptr;
+    hipEvent_t ev_snap = nullptr, ev_adone[2] = {nullptr, nullptr}, ev_bdone[2] = {nullptr, nullptr};
     uint64_t wait_ticks = 0;            // relation-owner ticket waits: wall-clock bound (engine_relowner.inc)
     hipStream_t stream = nullptr;
     int64_t device_bytes = 0;
@@ -181,6 +186,9 @@ struct kb2e_ctx {
     size_t rpar_wide_lds = 0;
     bool rpar_cons_gen = false;   // the same chain for FP32 and 112 < n <= 128 (kernels_transr_chaing.hpp)
     size_t rpar_gen_lds = 0;
+    bool rpar_widep = false;      // 128 < n <= 512: the whole step in kernels_transr_widep.hpp
+    WideGeom rpar_wg;             // (its tile / scan geometry and LDS sizes)
+    DevBuf rpar_wsc;              // its transRNorm chains' W_c images, a workgroup's each
     DevBuf rpar_pflag, rpar_cons_tile, rpar_cpairs, rpar_cnrows;
     DevBuf rpar_y, rpar_wpart, rpar_rpart, rpar_tile_act, rpar_pair, rpar_relpair, rpar_relpair_stamp, rpar_scan_pre, rpar_tiles,
         rpar_ntiles, rpar_tile_first, rpar_rel_begin, rpar_scan;
@@ -236,6 +244,9 @@ struct kb2e_ctx {
         if (ev_epoch_done) (void)hipEventDestroy(ev_epoch_done);
         if (ev_index) (void)hipEventDestroy(ev_index);
         if (side_stream) (void)hipStreamDestroy(side_stream);
+        if (suba_stream) (void)hipStreamDestroy(suba_stream);
+        for (hipEvent_t e : {ev_snap, ev_adone[0], ev_adone[1], ev_bdone[0], ev_bdone[1]})
+            if (e) (void)hipEventDestroy(e);
         if (fold_stream) (void)hipStreamDestroy(fold_stream);
         if (ev_fold_a) (void)hipEventDestroy(ev_fold_a);
         if (ev_fold_b) (void)hipEventDestroy(ev_fold_b);
@@ -1290,7 +1301,6 @@ kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out) {
         g.sub_batches > 64)
         return KB2E_EINVAL;
     if (g.model == KB2E_TRANSR && g.num_relations > g.num_entities) return KB2E_EINVAL;
-    if (g.schedule == KB2E_SCHEDULE_PARALLEL && g.model == KB2E_TRANSR && g.dim > 128) return KB2E_EUNSUPPORTED;  // entityVec_next_[relation]
     std::unique_ptr<kb2e_ctx> c(new kb2e_ctx());
     c->cfg = g;
     c->rng.seed_with(g.seed);

@@ -9,7 +9,8 @@
 // steps -- and bfgs() runs on the GPU through include/kb2e_engine.h.
 // GPU-only flags are additive: --precision 64|32, --device N, --transrcompat 0|1,
 // --schedule 0|1 (0 = ORDERED, the reference's sequence; 1 = PARALLEL, summed
-// per-row deltas with one norm per batch, kb2e_engine.h kb2e_schedule).
+// per-row deltas with one norm per batch, kb2e_engine.h kb2e_schedule), --gpus N,
+// --subbatches K (PARALLEL TransR: each batch applied in K sub-batches).
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -53,6 +54,7 @@ struct EmbeddingArguments {  // common/args.h:9-25, defaults common/constants.h:
     int transrCompat = 1;
     int schedule = 0;
     int gpus = 1;
+    int subBatches = 0;  // 0: the engine's default (kb2e_config.sub_batches)
 
     std::string to_string() const {  // common/args.cpp:33-50
         std::string r = "Options: [";
@@ -108,6 +110,7 @@ void printUsage(const char* invoked) {  // common/args.cpp:125-142
     printf("   --transrcompat [1] (TransR: reproduce the accumulating energy)\n");
     printf("   --schedule [0] (GPU: 0 ordered = the reference's sequence, 1 parallel)\n");
     printf("   --gpus [1] (GPU: devices --device .. --device+N-1, triples sharded by head, epoch merge over RCCL)\n");
+    printf("   --subbatches [engine default] (GPU, parallel TransR: each batch's updates in this many sub-batches)\n");
 }
 
 EmbeddingArguments parseArgs(int argc, char** argv) {  // common/args.cpp:53-122
@@ -134,6 +137,7 @@ EmbeddingArguments parseArgs(int argc, char** argv) {  // common/args.cpp:53-122
     if ((i = argpos("transrcompat", true, argc, argv)) != -1) a.transrCompat = atoi(argv[i + 1]);
     if ((i = argpos("schedule", true, argc, argv)) != -1) a.schedule = atoi(argv[i + 1]) ? 1 : 0;
     if ((i = argpos("gpus", true, argc, argv)) != -1) a.gpus = std::max(1, atoi(argv[i + 1]));
+    if ((i = argpos("subbatches", true, argc, argv)) != -1) a.subBatches = std::max(1, atoi(argv[i + 1]));
     return a;
 }
 
@@ -329,6 +333,7 @@ class Trainer {  // the interface of common::Trainer (common/trainer.h:14-78)
         cfg.device = (one && one[0] == '1') ? args_.device : args_.device + k;
         cfg.transr_compat = args_.transrCompat;
         cfg.schedule = args_.schedule ? KB2E_SCHEDULE_PARALLEL : KB2E_SCHEDULE_ORDERED;
+        if (args_.subBatches > 0) cfg.sub_batches = args_.subBatches;
         if (h.empty()) {
             printf("kb2e: GPU %d has no training triples (--gpus %d)\n", k, args_.gpus);
             exit(1);

@@ -16,10 +16,11 @@
 // sit between two walks.  The working matrix W_c lives in registers of waves
 // 1-3 as the MFMA B fragments of their column slices (slice cb on wave
 // 1 + cb % 3), so X's tiles read no B operand from LDS, and chunk k's update
-// W_c -= lr A_k^T G_k and its pair records are made by waves 1-3 at the start of
-// chunk k+1, while wave 0 walks chunk k+1, instead of between the two walks (a
-// wave touches only its own slices' columns of the P buffers, so reading G_k
-// and writing X_{k+2} into the same buffer need no barrier).  The walk keeps the chunk's projection
+// W_c -= lr A_k^T G_k is made by waves 1-3 at the start of chunk k+1, while wave
+// 0 walks chunk k+1, instead of between the two walks (a wave touches only its
+// own slices' columns of the P buffers, so reading G_k and writing X_{k+2} into
+// the same buffer need no barrier); the walker writes each violator's pair record
+// G to global memory as it publishes it, off the helpers' per-chunk work.  The walk keeps the chunk's projection
 // rows in registers (lane j: half l >> 5 of row j & 31), so a violator's
 // rank-1 move of the later rows is FMAs on registers with the violator's G row
 // read as LDS broadcasts.  The relation's last-update chunk starts after W_c's
@@ -183,8 +184,8 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
     bool changed = false;
     int32_t* const vio = bf.vio + (int64_t)g0 * kCPairs;  // the relation's violators (run * kCPairs >= its pairs)
     int nvt = 0;
-    // the chunk whose W_c update and pair records the helper waves still owe (nv 0: none)
-    int pend_nv = 0, pend_par = 0, pend_pc = 0, pend_ka = 0, pend_base = 0, pend_nvt = 0;
+    // the chunk whose W_c update the helper waves still owe (nv 0: none)
+    int pend_nv = 0, pend_par = 0, pend_pc = 0, pend_ka = 0;
     tick(0);
 
     // one 16 x 16 MFMA tile: rows rt of A (Ar) against rows cb of B (a Gram tile);
@@ -381,8 +382,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
         }
     };
     // the helper waves' debt: the pending chunk's W_c -= lr A^T G on their slices
-    // (its G rows in P buffer pend_pc, its rows in A slot pend_ka) and its pair records
-    // (each wave its own slices' columns; lanes of DPP row kq take violators kq, kq + 4, ...)
+    // (its G rows in P buffer pend_pc, its rows in A slot pend_ka)
     auto apply_pending = [&]() {
         if (w == 0 || pend_nv == 0) return;
         const T* Pp = Pbuf + pend_pc * R * L;
@@ -419,21 +419,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                     for (int s = 0; s < KS; ++s) reg[si * KS + s] = fma(ac[s], gc[si], reg[si * KS + s]);
                 }
         }
-        // the pair records: each helper its own slices' columns (the next chunk's
-        // projections overwrite the other slices' columns of this P buffer meanwhile)
-#pragma unroll
-        for (int si = 0; si < NSW; ++si) {
-            const int cb = hw + 3 * si;
-            if (cb >= NB) continue;
-            const int c = cb * 16 + l16;
-            for (int k = kq; k < ((bf.dbg & 8) ? 0 : pend_nv); k += 4) {
-                const int v = vl[k];
-                const int sl = ps[pend_base + v];
-                T* dst = sl >= 0 ? bf.pair + (int64_t)sl * ld : bf.relpair + (int64_t)r * ld;
-                if (c < n) dst[c] = Pp[v * L + c];
-                if (hw == 0 && si == 0 && l16 == 0) vio[pend_nvt + k] = sl;
-            }
-        }
+        // (the pair records G were written by the walker as it published each violator)
     };
     // the relation's last update renormalises W_c's rows before its own pairs'
     // shrinks (transr/trainer.cpp:178-180): row sums of the slices in DPP rows, then
@@ -605,6 +591,7 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                         const T pp = readlane_f(q, v);
                         const T aa = readlane_f(aaj, v);
                         const T cjv = Gm[j * LG + v];  // a_j . a_v for the later rows' update
+                        const int slv = ps[base + v];  // the violator's record slot (-2: (entity'[r], r))
                         // the violator's current row to LDS for the column-lane layout
                         if (j == v) {
 #pragma unroll
@@ -644,6 +631,11 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
                         const T g = c < n ? cpf * pv - cvf * (Vc + aa * pv) : T(0);
                         tick(9);
                         if (c < NP) P[v * L + c] = g;  // the violator's row now holds G
+                        {  // its pair record G (da = -lr W G with the final matrix: chain_records)
+                            T* dst = slv >= 0 ? bf.pair + (int64_t)slv * ld : bf.relpair + (int64_t)r * ld;
+                            if (c < n) dst[c] = g;
+                            if (l == 0) vio[nvt + npub] = slv;
+                        }
                         tick(10);
                         const bool upd = j > v && j < cc;
                         T qh = T(0);  // this lane's half of |p_j|^2
@@ -738,8 +730,6 @@ __global__ __launch_bounds__(kChainThreads) void transr_cons_pipe_kernel(RParArg
             pend_par = par;
             pend_pc = pc;
             pend_ka = ka;
-            pend_base = base;
-            pend_nvt = nvt;
             nvt += nv;
             if (vmask) changed = true;
             const bool restart = nbase == tail_start && changed && cn > 0;  // the tail: afresh

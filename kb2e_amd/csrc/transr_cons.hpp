@@ -27,10 +27,9 @@ void proj_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, hipStr
 // (kernels_transr_wave.hpp); needs bf.x, bf.d and the hinge decisions in place.
 template <typename T>
 void grad_wave_launch(const RParArgs& a, const RParBufs<T>& bf, int grid, hipStream_t stream);
-// transRNorm per relation, pair by pair, in chunks of 32 (kernels_transr_pipe.hpp, or
-// the unpipelined kernels_transr_seq.hpp under KB2E_RPAR_CHAIN=serial; FP64, n <= 64):
-// dynamic LDS bytes (and the kernel's limit raised to it); the launch, one workgroup per
-// relation, most frequent first (those absent from the batch exit), each making its
+// transRNorm per relation, pair by pair, in chunks of 32 (kernels_transr_pipe.hpp; FP64,
+// n <= 64): dynamic LDS bytes (and the kernel's limit raised to it); the launch, one
+// workgroup per relation of the batch (a.brel, most frequent first), each making its
 // relation's pair records at the end of its chain (chain_records).
 size_t cons_seq_setup(int n);
 void cons_seq_launch(const RParArgs& a, const RParBufs<double>& bf, size_t lds, hipStream_t stream);
@@ -58,5 +57,30 @@ bool cons_chainw_pipelined(int n);
 void cons_seq_take_stats(unsigned long long (&st)[64]);
 // Adds the kernel's round statistics (g_rpar_rounds layout) to st and resets them.
 void cons_wave_take_stats(unsigned long long (&st)[16]);
+
+// The whole PARALLEL TransR step at 128 < n <= 512, FP64 and FP32 (kernels_transr_widep.hpp,
+// transr_wide.hip): matrices from global memory, CP = ceil(n / 128) element pairs a lane.
+constexpr int kWideParMaxN = 512;
+struct WideGeom {
+    int St = 1;             // samples a tile (the tile kernel's LDS within 150 KiB)
+    int chunk = 2;          // compat scan: calls a chunk
+    size_t tile_lds = 0, scan_lds = 0, chain_lds = 0;
+};
+bool wide_par_supported(int n);
+// Chooses the geometry for (n, ld, element size) and raises the kernels' LDS limits.
+WideGeom wide_setup(int n, int ld, int esize);
+// Phase A (reads the tables bf names): fixed energy -- the tile kernel (energies,
+// hinge, directions, partials) and the pair-dedupe inserts; compat -- projections,
+// the work-vector scan (scan: chunk sums, scan_pre: their prefix; work_in -> work_out)
+// with the hinge, then the partials.
+template <typename T>
+void wide_phase_a(const RParArgs& a, const RParBufs<T>& bf, const WideGeom& g, int tgrid, double* scan,
+                  double* scan_pre, const double* work_in, double* work_out, hipStream_t st);
+// Phase B: relation rows, entity rows, then (constraint) transRNorm pair by pair per
+// relation (wsc: a min(nr, B) x n x ld double scratch, a workgroup's W_c each) and the
+// entity rows' pair records.
+template <typename T>
+void wide_phase_b(const RParArgs& a, const RParBufs<T>& bf, const WideGeom& g, double* wsc, bool constraint,
+                  int rel_segs_max, hipStream_t st);
 
 }  // namespace kb2e

@@ -90,9 +90,9 @@ def _cons_form(dim, mfma):
     kernels_transr_chainw.hpp elsewhere -- unless
     KB2E_RPAR_CONS picks the Jacobi tile / wave kernels; Jacobi above 112."""
     ck = os.environ.get("KB2E_RPAR_CONS", "")
-    if ck in ("tile", "jacobi"):
+    if ck in ("tile", "jacobi") and dim <= 128:
         return "jacobi"
-    assert dim <= 128, "PARALLEL TransR trains n <= 128"
+    assert dim <= 512, "PARALLEL TransR trains n <= 512"
     return "chunk1"
 
 
@@ -311,14 +311,51 @@ def test_transr_parallel_generic_chain_windows(monkeypatch):
     _transr_vs_model(data.synthetic("small", seed=1), 50, 1, monkeypatch, St=8, compat=True, rate=0.001)
 
 
-def test_transr_parallel_refuses_above_128(monkeypatch):
-    """PARALLEL TransR trains n <= 128 (the VALU tile path holds two elements a
-    lane); wider contexts are refused (KB2E_EUNSUPPORTED: the ORDERED schedule
-    trains every dim a context takes, up to 512)."""
+@pytest.mark.parametrize("dim,compat,St_cap", [(160, False, 8), (160, True, 8), (260, False, 8), (260, True, 2),
+                                               (384, False, 8), (512, True, 8)])
+def test_transr_parallel_wide(dim, compat, St_cap, monkeypatch):
+    """128 < n <= 512 (kernels_transr_widep.hpp: every matrix from global memory,
+    up to four element pairs a lane): the same model as the narrower kernels --
+    summed gradient step, then transRNorm pair by pair per relation (cons =
+    "chunk1") -- against oracle/parallel.py, both energies, two epochs of the tiny
+    set (several chunks and violators a relation); St_cap caps the tile size below
+    the LDS-bounded choice (several tiles a relation)."""
+    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St_cap, compat=compat, mfma=False)
+
+
+@pytest.mark.parametrize("sub,prefix", [(1, "0"), (1, "1"), (3, "0"), (3, "1")])
+def test_transr_parallel_wide_compat_scan(sub, prefix, monkeypatch):
+    """The wide kernels' compat scan in both forms (KB2E_RPAR_SCAN_PREFIX: the chunks'
+    prefix made once, or summed by every chunk block), whole batches and sub-batches
+    (phase A on the start-of-batch copies), n = 200."""
+    monkeypatch.setenv("KB2E_RPAR_SCAN_PREFIX", prefix)
+    _transr_vs_model(tiny(), 200, 2, monkeypatch, St=4, compat=True, mfma=False, sub=sub)
+
+
+def test_transr_parallel_wide_fp32_close():
+    """FP32 tables at n = 200 on the wide kernels: loss and active counts within 1 %
+    of the FP64 run over two epochs (FP32 hinge decisions flip at the margin)."""
+    ds = data.synthetic("small", seed=1)
+    out = {}
+    for prec in (64, 32):
+        eng = Engine("R", 200, ds.num_entities, ds.num_relations, rate=0.001, batches=10, seed=3, precision=prec,
+                     schedule="parallel", transr_compat=False)
+        eng.upload_triples(ds.train)
+        e0, r0, _ = eng.init_params()
+        eng.transr_seed(e0, r0)
+        out[prec] = [eng.train_epoch() for _ in range(2)]
+        eng.close()
+    for (l64, a64), (l32, a32) in zip(out[64], out[32]):
+        assert abs(a64 - a32) <= 0.01 * a64 and abs(l64 - l32) <= 0.01 * l64
+
+
+def test_transr_parallel_refuses_above_512():
+    """Every --size up to the engine's cap trains PARALLEL; wider contexts are refused
+    at creation (KB2E_EINVAL, as for every model)."""
     from kb2e_amd.engine import EngineError
     ds = tiny()
-    with pytest.raises(EngineError, match="EUNSUPPORTED"):
-        Engine("R", 136, ds.num_entities, ds.num_relations, schedule="parallel")
+    with pytest.raises(EngineError, match="EINVAL"):
+        Engine("R", 513, ds.num_entities, ds.num_relations, schedule="parallel")
 
 
 def test_transr_parallel_fp32_chain_close(monkeypatch):

@@ -15,6 +15,7 @@
 #   bash tools/gpu.sh k5stats  <tag> <chain> [chain ...]      K5 chain phase counters per KB2E_RPAR_CHAIN ("-" = unset;
 #                                                           CFG=<config> for another bench config)
 #   bash tools/gpu.sh timeline <tag>                        kernel timeline of the driver-style line (K=20)
+#   bash tools/gpu.sh pmcw     <tag>                        TransH phase-B kernels' SQ counters (occupancy, LDS, waits)
 # (ab: AB_EPOCH=1 also times the whole epoch and epoch 50, e.g. the TransH gate sweep
 #  AB_EPOCH=1 bash tools/gpu.sh ab gate transh_fb15k KB2E_HPAR_ORTH_MIN 0 16 64 256)
 set -o pipefail
@@ -87,6 +88,15 @@ PY
         -T -d "$OUT/pmc_MFMA" -o run --output-format csv -- \
         python3 bench.py $PASS "$@" > "$OUT/pmc_MFMA.log" 2>&1 || fail "pmc MFMA" $? "$OUT/pmc_MFMA.log"
     echo profile done ;;
+  pmcw)  # TransH phase B split into its kernels (KB2E_HPAR_FUSE=0): SQ counters per kernel family
+    export KB2E_HPAR_FUSE=0
+    PASS="--config transh_fb15k --only --no-cpu-baseline --no-epoch --steps 100 --warmup 20"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/trace" -o run --output-format csv -- \
+        python3 bench.py $PASS > "$OUT/trace.log" 2>&1 || fail trace $? "$OUT/trace.log"
+    timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAIT_INST_ANY \
+        SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS -T -d "$OUT/pmc_SQ" -o run --output-format csv -- \
+        python3 bench.py $PASS > "$OUT/pmc_SQ.log" 2>&1 || fail "pmc SQ" $? "$OUT/pmc_SQ.log"
+    python3 tools/pmc_table.py "$OUT/pmc_SQ/run_counter_collection.csv" > "$OUT/pmc_SQ.txt" && cat "$OUT/pmc_SQ.txt" ;;
   envelope)
     MODEL=$1; DIM=$2; COMPAT=$3; EP=$4; SEEDS=$5; NB=${6:-100}; SCH=${7:-ordered,parallel}; SUB=${8:-}
     timeout -k 10 1150 python -u tools/seed_envelope.py --model "$MODEL" --dim "$DIM" --compat "$COMPAT" --epochs "$EP" \
