@@ -87,8 +87,11 @@ typedef struct {
                                update directions stay on the start-of-batch tables,
                                common/trainer.cpp:132-133); nearer the reference's
                                norm after every update (transr/trainer.cpp:174-187).
-                               1 = one per batch.  Ignored by the other models and the
-                               ORDERED schedule. */
+                               1 = one per batch; 0 (kb2e_default_config) = by width:
+                               the smallest count whose loss stays inside the
+                               reference's seed envelope where measured (2 for
+                               dim <= 64, 4 above).  Ignored by the other
+                               models and the ORDERED schedule. */
 } kb2e_config;
 
 typedef struct kb2e_ctx kb2e_ctx;
@@ -97,6 +100,9 @@ typedef struct kb2e_ctx kb2e_ctx;
 void kb2e_default_config(kb2e_config* cfg);
 
 kb2e_status kb2e_create(const kb2e_config* cfg, kb2e_ctx** out);
+/* The context's configuration with the defaults resolved (sub_batches 0 -> the
+ * count the context runs). */
+kb2e_status kb2e_get_config(const kb2e_ctx* ctx, kb2e_config* out);
 void kb2e_destroy(kb2e_ctx* ctx);
 const char* kb2e_last_error(const kb2e_ctx* ctx);
 

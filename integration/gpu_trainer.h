@@ -66,6 +66,7 @@ class GpuTrainer final : public Base {
         c.schedule = env_int("KB2E_SCHEDULE", KB2E_SCHEDULE_ORDERED);
         c.device = env_int("KB2E_DEVICE", 0);
         c.transr_compat = env_int("KB2E_TRANSR_FIXED", 0) ? 0 : 1;
+        c.sub_batches = env_int("KB2E_SUB_BATCHES", c.sub_batches);  // PARALLEL TransR only
         check(kb2e_create(&c, &ctx_), "kb2e_create");
         const int64_t n = (int64_t)this->heads_.size();
         check(kb2e_upload_triples(ctx_, this->heads_.data(), this->tails_.data(), this->relations_.data(), n),

@@ -28,7 +28,7 @@ EXPORTS = [
     "kb2e_device_bytes", "kb2e_device_tables", "kb2e_renormalize", "kb2e_evaluate", "kb2e_evaluate_transr_compat",
     "kb2e_renormalize_rows", "kb2e_init_params_device", "kb2e_write_table", "kb2e_format_table",
     "kb2e_read_table", "kb2e_comm_unique_id", "kb2e_comm_init_rank", "kb2e_comm_init_group", "kb2e_merge_epoch",
-    "kb2e_merge_epoch_group", "kb2e_comm_info",
+    "kb2e_merge_epoch_group", "kb2e_comm_info", "kb2e_get_config",
 ]
 COMM_ID_BYTES = 128
 READ_VERBATIM, READ_UNIT, READ_SHRINK = 0, 1, 2
@@ -57,6 +57,7 @@ def lib():
         sig = {
             "kb2e_default_config": (None, [C.POINTER(Config)]),
             "kb2e_create": (i32, [C.POINTER(Config), C.POINTER(vp)]),
+            "kb2e_get_config": (i32, [vp, C.POINTER(Config)]),
             "kb2e_destroy": (None, [vp]),
             "kb2e_last_error": (C.c_char_p, [vp]),
             "kb2e_upload_triples": (i32, [vp, i32p, i32p, i32p, i64]),
@@ -130,14 +131,15 @@ class Engine:
         cfg.num_batches, cfg.seed, cfg.precision, cfg.sampler = batches, seed, precision, sampler
         cfg.transr_compat, cfg.device = int(transr_compat), device
         cfg.schedule = SCHEDULES[schedule] if isinstance(schedule, str) else int(schedule)
-        if sub_batches is not None:  # (None: the engine's default, kb2e_default_config)
+        if sub_batches is not None:  # (None: the engine's default by width, kb2e_default_config)
             cfg.sub_batches = int(sub_batches)
-        self.cfg = cfg
         h = C.c_void_p()
         st = lib().kb2e_create(C.byref(cfg), C.byref(h))
         if st != 0:
             raise EngineError(f"kb2e_create failed: {STATUS.get(st, st)}")
         self.h = h
+        self.cfg = Config()  # the context's own, defaults resolved (kb2e_get_config)
+        self._check(lib().kb2e_get_config(self.h, C.byref(self.cfg)), "kb2e_get_config")
 
     def _check(self, st, what):
         if st != 0:

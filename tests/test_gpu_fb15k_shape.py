@@ -9,7 +9,8 @@ of 4,831 samples), trained for a few batches against the oracle.
   against oracle/orc.c, the restatement pinned bit-exact to the compiled
   reference: identical hinge-active counts per batch, loss to 1e-9 relative,
   every table within F64_ATOL_COUPLED.
-* PARALLEL against its CPU model (oracle/parallel.py) on the same glibc sample
+* PARALLEL (TransR: the default two sub-batches) against its CPU model
+  (oracle/parallel.py) on the same glibc sample
   stream: identical active counts, loss 1e-9, tables 1e-9.
 
 At this shape the paths that the 30k-triple sets do not reach switch on: hot
@@ -144,7 +145,7 @@ def test_fb15k_shape_parallel_vs_model(fb, transr_init, transh_warm, name):
                 lo, ao = transh_parallel_batches(pe, pr, pw, *args, rate=RATE, state=state, orth_rel_min=ORTH_REL_MIN)
             else:
                 lo, ao = transr_parallel_batches(pe, pr, pw, *args, rate=RATE, l1=True, compat=compat, work=work,
-                                                 St=8, cons="chunk1")
+                                                 St=8, cons="chunk1", sub=eng.cfg.sub_batches)  # (the default)
             eng.train_batches(1)
             lg, ag = eng.take_stats()
             assert ag == ao, (b, ag, ao)

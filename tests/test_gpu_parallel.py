@@ -496,6 +496,18 @@ def test_transr_parallel_sub_batches(dim, compat, mfma, St, sub, monkeypatch):
     _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=compat, mfma=mfma, sub=sub)
 
 
+@pytest.mark.parametrize("dim,compat,mfma,St,sub,batches", [(50, True, True, 8, 2, 9), (50, True, True, 8, 3, 7),
+                                                             (20, True, True, 4, 4, 9), (33, True, False, 4, 2, 9),
+                                                             (100, True, False, 8, 2, 9), (100, True, True, 8, 4, 9),
+                                                             (160, True, True, 8, 2, 9), (50, False, True, 8, 2, 9)])
+def test_transr_parallel_sub_batches_ragged(dim, compat, mfma, St, sub, batches, monkeypatch):
+    """Batches that `sub` does not divide (333 samples at 9 batches, 428 at 7: the
+    last sub-batch shorter, as on the FB15k-shaped set's 4,831): the compat scan
+    of a sub-batch covers its own calls only, so the carried work vectors the
+    next batch starts from are the reference's."""
+    _transr_vs_model(tiny(), dim, 2, monkeypatch, St=St, compat=compat, mfma=mfma, sub=sub, batches=batches)
+
+
 def test_transr_parallel_sub_batches_small_set(monkeypatch):
     """Sub-batches on the 30k-triple set (a hot relation of ~700 samples a batch:
     several chunks and windows a sub-batch), compat energy, n = 50."""
