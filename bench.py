@@ -358,6 +358,8 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
         dist.all_reduce(row, op=dist.ReduceOp.SUM)
         comm = [{"rank": int(x[1]), "comm_nranks": int(x[0]), "entity_block": [int(x[2]), int(x[3])],
                  "device": int(x[4]), "pci_bus_id": int(x[5])} for x in row.tolist()]
+    # PARALLEL TransR runs each batch as `sub_batches` phase-A / phase-B launch pairs,
+    # each over B / sub_batches samples (the roofline's units per launch below)
     sub_batches = eng.cfg.sub_batches if model == "R" and schedule == "parallel" else 1
     eng.close()
     samples = steps * B
@@ -377,10 +379,11 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
     s = 8 if args.precision == 64 else 4
     score_b, fold_b = phase_bytes(model, dim, s, a)
     per_sample = score_b + fold_b
+    units = B / sub_batches  # samples one launch (span) processes
     if fold_ms >= score_ms:
-        dominant, avg_ms, bytes_per_launch = fold_name, fold_ms / max(1, fold_n), fold_b * B
+        dominant, avg_ms, bytes_per_launch = fold_name, fold_ms / max(1, fold_n), fold_b * units
     else:
-        dominant, avg_ms, bytes_per_launch = "score", score_ms / max(1, score_n), score_b * B
+        dominant, avg_ms, bytes_per_launch = "score", score_ms / max(1, score_n), score_b * units
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     # HBM bytes per launch from the PMC counters (FETCH_SIZE + WRITE_SIZE): counter
     # passes cannot share this timed run (separate rocprofv3 --pmc runs,
@@ -433,6 +436,7 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
                      "traffic_frac": traffic / (avg_ms * 1e-3) / 1e9 / PEAK_HBM_GBS if traffic and avg_ms > 0 else None,
                      "kernel": dominant,
                      "kernel_avg_us": avg_ms * 1e3, "algorithmic_bytes_per_launch": bytes_per_launch,
+                     "samples_per_launch": units,
                      "kernels_avg_us": kernels_us, "step_achieved_GBs": per_sample * samples / elapsed / 1e9},
     }
 

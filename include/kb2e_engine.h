@@ -90,7 +90,7 @@ typedef struct {
                                1 = one per batch; 0 (kb2e_default_config) = by width:
                                the smallest count whose loss stays inside the
                                reference's seed envelope where measured (2 for
-                               dim <= 64, 4 above).  Ignored by the other
+                               dim <= 64, 3 above).  Ignored by the other
                                models and the ORDERED schedule. */
 } kb2e_config;
 

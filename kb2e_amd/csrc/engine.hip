@@ -1293,12 +1293,12 @@ void kb2e_default_config(kb2e_config* cfg) {
 namespace {
 // PARALLEL TransR sub-batches when kb2e_config.sub_batches is 0: the smallest count
 // whose paired loss interval against the reference's seed envelope covers 0 at the
-// widths measured (FB15k-shaped, compat, 5 seeds): n = 50 -> 2
-// (k = 1: -2.8 % [-4.3, -1.4]; k = 2: -1.5 % [-5.3, +2.3]), n = 100 -> 4
-// (k = 2: -3.5 % [-5.9, -1.1]; k = 4: -0.7 % [-1.6, +0.2]); wider: 4 (unmeasured)
+// widths measured (FB15k-shaped, compat, 100 batches, 5 seeds):
+// n = 50 -> 2 (k = 1: -2.8 % [-4.3, -1.4]; k = 2: -0.8 % [-2.5, +0.9]), n = 100 -> 3
+// (k = 2: -3.7 % [-5.4, -2.0]; k = 3: -1.8 % [-3.8, +0.1]); wider: 3 (unmeasured)
 int32_t default_sub_batches(const kb2e_config& g) {
     if (g.model != KB2E_TRANSR || g.schedule != KB2E_SCHEDULE_PARALLEL) return 1;
-    return g.dim <= 64 ? 2 : 4;
+    return g.dim <= 64 ? 2 : 3;
 }
 }  // namespace
 

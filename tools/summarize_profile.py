@@ -93,6 +93,10 @@ def main(src, tag, config, prec, schedule="parallel", batches="200"):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
     bench = open(os.path.join(src, "bench.json")).read().strip()
+    # PARALLEL TransR sub-batches: a phase-A / phase-B launch pair per sub-batch, so a
+    # phase's bytes per launch are its bytes per batch over the sub-batch count
+    sub = int(json.loads(bench).get("config", {}).get("sub_batches", 1) or 1)
+    nbatch *= sub
     pmc = {}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         path = os.path.join(src, f"pmc_{c}", "run_counter_collection.csv")
@@ -110,7 +114,7 @@ def main(src, tag, config, prec, schedule="parallel", batches="200"):
             for q in (p.split("|") if p else []):
                 ph[q] += float(r["Counter_Value"])
         pmc[c] = {k: v[0] / max(1, v[1]) for k, v in agg.items()}  # KiB per launch
-        pmc[c + "_phase"] = {k: v / nbatch for k, v in ph.items()}  # KiB per batch
+        pmc[c + "_phase"] = {k: v / nbatch for k, v in ph.items()}  # KiB per launch (batch or sub-batch)
     per_kernel = {}
     for fam in set(pmc.get("FETCH_SIZE", {})) | set(pmc.get("WRITE_SIZE", {})):
         f = pmc.get("FETCH_SIZE", {}).get(fam, 0.0) * 1024
@@ -120,7 +124,7 @@ def main(src, tag, config, prec, schedule="parallel", batches="200"):
         f = pmc.get("FETCH_SIZE_phase", {}).get(p, 0.0) * 1024
         w = pmc.get("WRITE_SIZE_phase", {}).get(p, 0.0) * 1024
         per_kernel[p] = {"fetch_bytes_raw": f, "write_bytes": w, "hbm_bytes_per_launch": 2 * f + w,
-                         "note": "phase total per batch"}
+                         "note": f"phase total per launch ({sub} a batch)"}
     mf = mfma_table(src, stats)
     if mf:
         per_kernel["mfma_f64"] = mf
