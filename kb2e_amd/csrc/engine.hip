@@ -98,7 +98,7 @@ struct kb2e_ctx {
     // suba_stream beside phase B of sub-batch j) and the events that order them
     DevBuf sb_x, sb_d, sb_y, sb_wpart, sb_rpart, sb_pflag, sb_cons_tile, sb_cpairs, sb_vio, sb_cnrows;
     hipStream_t suba_stream = nullptr;
-    hipEvent_t ev_snap = nullptr, ev_adone[2] = {nullptr, nullptr}, ev_bdone[2] = {nullptr, nullptr};
+    hipEvent_t ev_adone[2] = {nullptr, nullptr}, ev_bdone[2] = {nullptr, nullptr};
     uint64_t wait_ticks = 0;            // relation-owner ticket waits: wall-clock bound (engine_relowner.inc)
     hipStream_t stream = nullptr;
     int64_t device_bytes = 0;
@@ -168,6 +168,7 @@ struct kb2e_ctx {
     DevBuf hpar_ids;                       // ... and a flagged sample's ids [B][8]
     DevBuf hpar_tag;                       // PARALLEL TransH: per entity, the relations its flagged pairs have
     uint32_t hpar_stamp = 0;
+    DevBuf hpar_clk;                       // KB2E_HPAR_CLK: the w-apply workgroups' clocks (diagnostic)
     DevBuf hpar_count;                     // PARALLEL TransH: normOrth iterations of the last two batches, relation passes run
     uint32_t hpar_orth_min = 0;            // ... from which normOrth takes the relation pass
     int32_t hpar_orth_q = 0;               // the one-wave pass's second-sweep queue (kOrthQ)
@@ -245,7 +246,7 @@ struct kb2e_ctx {
         if (ev_index) (void)hipEventDestroy(ev_index);
         if (side_stream) (void)hipStreamDestroy(side_stream);
         if (suba_stream) (void)hipStreamDestroy(suba_stream);
-        for (hipEvent_t e : {ev_snap, ev_adone[0], ev_adone[1], ev_bdone[0], ev_bdone[1]})
+        for (hipEvent_t e : {ev_adone[0], ev_adone[1], ev_bdone[0], ev_bdone[1]})
             if (e) (void)hipEventDestroy(e);
         if (fold_stream) (void)hipStreamDestroy(fold_stream);
         if (ev_fold_a) (void)hipEventDestroy(ev_fold_a);

@@ -57,6 +57,8 @@ struct HParArgs {
     uint32_t orth_rel_min;
     uint32_t* orth_rel_runs;    // batches whose relation pass ran (kb2e_counter "transh_orth_rel_batches")
     int32_t orth_q;             // second-sweep queue capacity (kOrthQ; KB2E_HPAR_ORTH_Q for the tests)
+    unsigned long long* clk;    // KB2E_HPAR_CLK (diagnostic): per w-apply workgroup start, after its small
+                                // segments, end (wall clock), large segments << 32 | their events
 };
 
 // The flagged entity rows' relations this batch: the first relation a row is
@@ -87,8 +89,13 @@ __device__ __forceinline__ bool orth_shared(HParArgs<T> a, int e) {
 // have a few events: a 16-wave workgroup each was 1,345 workgroups a batch, bound
 // by dispatch, ~30 us).  A segment of at most kWSmall events is one wave's: its sum
 // in event order, the unit norm, the store.  The larger ones (the hot relations)
-// take the whole workgroup one after another: the waves take G events at a time
-// round-robin, partial sums combined in wave order, wave 0 applies.
+// take the whole workgroup one after another: each wave sums a contiguous slice of
+// the segment's events, the partial sums are combined in wave order, wave 0 applies.
+// The kernel is a chain of dependent memory round trips on few waves (r23 PMC,
+// 1.3 waves a SIMD, 2 LDS instructions a wave, no bank conflicts,
+// SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY = 0.56), so every step keeps its loads
+// together: the w row is loaded with the segment's first event records, a wave's
+// event records (up to 64) in one load, their delta rows 16 at a time.
 constexpr int kWSmall = 32;
 
 template <typename T, int CH, int NWV>
@@ -99,55 +106,59 @@ __device__ __forceinline__ void transh_w_apply_body(HParArgs<T> a, int bid) {
     const int se = min(sb + NWV, a.batch_seg[a.batch + 1]);
     if (sb >= se) return;
     const int w = threadIdx.x >> 6, l = lane_id();
+    const unsigned long long t_start = a.clk ? wall_clock64() : 0ull;
+    unsigned long long n_large = 0;
     constexpr int G = 16 / CH;
-    // the active events of [base, base + G) ∩ [p0, p1) (lanes < G) added to acc, their
-    // delta rows (score kernel) in flight together, summed in event order
-    auto add_events = [&](int base, int p1, T (&acc)[CH][kVec]) {
-        const int p = base + l;
+    // the active events of [q0, q1) (at most 64: one record a lane) added to acc in
+    // event order, G delta rows (score kernel) in flight at a time
+    auto add_events = [&](int q0, int q1, T (&acc)[CH][kVec]) {
+        const int p = q0 + l;
         int xrow = -1;
-        if (l < G && p < p1) {
+        if (p < q1) {
             const int32_t meta = a.meta[p];
             if (((meta & 3) - 1) != 0) xrow = meta >> 4;  // active update: kk * 2 + u
         }
         uint64_t m = __ballot(xrow >= 0);
         const bool act = m != 0;
-        int ev[G], xr[G];
-        int ne4 = 0;
-        for (; ne4 < G && m; ++ne4) {
-            ev[ne4] = __builtin_ctzll(m);
-            m &= m - 1;
-            xr[ne4] = readlane_i32(xrow, ev[ne4]);
-        }
-        T dv[G][CH][kVec];
+        while (m) {
+            // G rows a round, every load unconditional (a missing event reads the round's
+            // first row again and adds nothing): the loads issue back to back -- loads
+            // behind a per-row condition were each waited for before the next one went
+            // out, a memory round trip per event (KB2E_HPAR_CLK: the hot relation's
+            // 1,140 events took 25 us)
+            int xr[G];
 #pragma unroll
-        for (int q = 0; q < G; ++q) {
-            if (q >= ne4) continue;
-            const T* drow = a.snap + (int64_t)xr[q] * a.ld;
+            for (int q = 0; q < G; ++q) {
+                xr[q] = m ? readlane_i32(xrow, __builtin_ctzll(m)) : -1;
+                m &= m - 1;
+            }
+            T dv[G][CH][kVec];
 #pragma unroll
-            for (int cc = 0; cc < CH; ++cc)
+            for (int q = 0; q < G; ++q) {
+                const T* drow = a.snap + (int64_t)(xr[q] >= 0 ? xr[q] : xr[0]) * a.ld;
 #pragma unroll
-                for (int k = 0; k < kVec; ++k) {
-                    const int el = cc * (kWave * kVec) + l * kVec + k;
-                    dv[q][cc][k] = el < a.n ? drow[el] : T(0);
-                }
-        }
+                for (int cc = 0; cc < CH; ++cc)
 #pragma unroll
-        for (int q = 0; q < G; ++q) {
-            if (q >= ne4) continue;
+                    for (int k = 0; k < kVec; ++k) {
+                        const int el = cc * (kWave * kVec) + l * kVec + k;
+                        dv[q][cc][k] = el < a.n ? drow[el] : T(0);
+                    }
+            }
 #pragma unroll
-            for (int cc = 0; cc < CH; ++cc)
+            for (int q = 0; q < G; ++q) {
+                if (xr[q] < 0) continue;
 #pragma unroll
-                for (int k = 0; k < kVec; ++k)
-                    if (elem_valid(cc, k, a.n)) acc[cc][k] += dv[q][cc][k];
+                for (int cc = 0; cc < CH; ++cc)
+#pragma unroll
+                    for (int k = 0; k < kVec; ++k)
+                        if (elem_valid(cc, k, a.n)) acc[cc][k] += dv[q][cc][k];
+            }
         }
         return act;
     };
-    // w_r += the sum, unit norm (a relation is touched only through an active update)
-    auto apply = [&](int s, const T (&sum)[CH][kVec]) {
-        const int r = a.seg_row[s] - a.ne;
-        RowReg<T, CH> W;
-        T* wrow = a.w + (int64_t)r * a.ld;
-        W.load(wrow, a.n);
+    // w_r += the sum, unit norm (a relation is touched only through an active update);
+    // W holds the row, loaded ahead
+    auto apply = [&](RowReg<T, CH>& W, T* wrow, const T (&sum)[CH][kVec]) {
 #pragma unroll
         for (int cc = 0; cc < CH; ++cc)
 #pragma unroll
@@ -161,21 +172,34 @@ __device__ __forceinline__ void transh_w_apply_body(HParArgs<T> a, int bid) {
         if (s < se) {
             const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
             if (p1 - p0 <= kWSmall) {
+                T* wrow = a.w + (int64_t)(a.seg_row[s] - a.ne) * a.ld;
+                RowReg<T, CH> W;
+                W.load(wrow, a.n);  // (beside the event records)
                 T acc[CH][kVec] = {};
-                bool act = false;
-                for (int base = p0; base < p1; base += G) act |= add_events(base, p1, acc);
-                if (act) apply(s, acc);
+                const bool act = add_events(p0, p1, acc);
+                if (act) apply(W, wrow, acc);
             }
         }
+    }
+    if (a.clk && threadIdx.x == 0) {
+        a.clk[4 * bid] = t_start;
+        a.clk[4 * bid + 1] = wall_clock64();
     }
     for (int s = sb; s < se; ++s) {  // the large ones, all waves (uniform: every wave sees the sizes)
         const int p0 = a.seg_start[s], p1 = a.seg_start[s + 1];
         if (p1 - p0 <= kWSmall) continue;
+        n_large += (1ull << 32) | (unsigned long long)(p1 - p0);
         if (threadIdx.x == 0) any = 0;
         __syncthreads();
+        T* wrow = a.w + (int64_t)(a.seg_row[s] - a.ne) * a.ld;
+        RowReg<T, CH> W;
+        if (w == 0) W.load(wrow, a.n);
+        // wave w: events [p0 + w S, p0 + (w + 1) S), 64 records a load
+        const int S = (p1 - p0 + NWV - 1) / NWV;
+        const int q0 = p0 + w * S, q1 = min(p1, q0 + S);
         T acc[CH][kVec] = {};
         bool act = false;
-        for (int base = p0 + w * G; base < p1; base += NWV * G) act |= add_events(base, p1, acc);
+        for (int q = q0; q < q1; q += kWave) act |= add_events(q, min(q1, q + kWave), acc);
 #pragma unroll
         for (int cc = 0; cc < CH; ++cc)
 #pragma unroll
@@ -191,9 +215,13 @@ __device__ __forceinline__ void transh_w_apply_body(HParArgs<T> a, int bid) {
                     sum[cc][k] = part[0][cc * kVec + k][l];
                     for (int v = 1; v < NWV; ++v) sum[cc][k] += part[v][cc * kVec + k][l];
                 }
-            apply(s, sum);
+            apply(W, wrow, sum);
         }
         __syncthreads();  // (part and any: the next large segment's)
+    }
+    if (a.clk && threadIdx.x == 0) {
+        a.clk[4 * bid + 2] = wall_clock64();
+        a.clk[4 * bid + 3] = n_large;
     }
 }
 
