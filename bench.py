@@ -391,7 +391,7 @@ def measure(args, schedule, ds, train, rank, world, local, dist, steps, warmup, 
     # same command, named in traffic_source
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}_{schedule}_f{args.precision}.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and args.dim is None:  # (the committed counters are the config's own width)
         try:
             fams = json.load(open(pmc))
             v = fams.get(dominant, {}).get("hbm_bytes_per_launch")
@@ -473,7 +473,12 @@ def main():
     ap.add_argument("--seed-epochs", type=int, default=SEED_EPOCHS)
     ap.add_argument("--late-epoch", type=int, default=LATE_EPOCH,
                     help="also time the whole epoch with this index (steady state); 0: skip")
+    ap.add_argument("--dim", type=int, default=None,
+                    help="another embedding width on the config's data (A/B lines, e.g. the n > 128 wide path)")
     args = ap.parse_args()
+    if args.dim is not None:  # (the config's model and data at another width; named in config.dim)
+        m_, sh_, _, me_, di_, ra_ = CONFIGS[args.config]
+        CONFIGS[args.config] = (m_, sh_, args.dim, me_, di_, ra_)
     if args.gpus < 1:
         sys.exit(f"bench.py: --gpus {args.gpus}: need at least one GPU")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:

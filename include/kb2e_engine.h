@@ -247,7 +247,8 @@ kb2e_status kb2e_profile_query(kb2e_ctx* ctx, const char* name, double* total_ms
  * alone.  KB2E_EINVAL for an unknown name. */
 kb2e_status kb2e_counter(kb2e_ctx* ctx, const char* name, int64_t* value);
 
-/* Device memory footprint in bytes (tables + work buffers). */
+/* Device memory the context holds, in bytes: every device buffer it has allocated
+ * and not freed (tables, epoch streams and index, exports, merge state). */
 int64_t kb2e_device_bytes(const kb2e_ctx* ctx);
 
 /* Multi-GPU epoch merge (the reference is single-process, so

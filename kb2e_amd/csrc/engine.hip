@@ -80,6 +80,9 @@ void run_batch_transh_parallel(kb2e_ctx* c, int64_t b);
 }  // namespace
 
 struct kb2e_ctx {
+    // live DevBuf bytes charged to this context (DevBuf::tally; first, so it outlives
+    // every buffer member's destructor)
+    int64_t device_bytes = 0;
     kb2e_config cfg{};
     std::string err;
     GlibcRand rng{1};
@@ -101,7 +104,6 @@ struct kb2e_ctx {
     hipEvent_t ev_adone[2] = {nullptr, nullptr}, ev_bdone[2] = {nullptr, nullptr};
     uint64_t wait_ticks = 0;            // relation-owner ticket waits: wall-clock bound (engine_relowner.inc)
     hipStream_t stream = nullptr;
-    int64_t device_bytes = 0;
 
     // tables (real_t = double or float by cfg.precision)
     DevBuf ent, rel, w;
@@ -357,9 +359,17 @@ kb2e_status fail(kb2e_ctx* c, kb2e_status s, const std::string& msg) {
     return s;
 }
 
+// the device buffers an entry point allocates are charged to its context
+struct TallyScope {
+    int64_t* prev;
+    explicit TallyScope(int64_t* t) : prev(DevBuf::tally_now) { DevBuf::tally_now = t; }
+    ~TallyScope() { DevBuf::tally_now = prev; }
+};
+
 template <class F>
 kb2e_status guarded(kb2e_ctx* c, F&& f) {
     if (!c) return KB2E_EINVAL;
+    TallyScope ts(&c->device_bytes);
     try {
         return f();
     } catch (const HipError& e) {
@@ -1097,7 +1107,6 @@ void setup_buffers(kb2e_ctx* c) {
         c->wsnap.alloc(c->w.bytes);
         memset_sync(c->wsnap.p, 0, c->wsnap.bytes);
     }
-    c->device_bytes = (int64_t)(c->ent.bytes + c->rel.bytes + c->w.bytes);
 }
 
 void setup_epoch_buffers(kb2e_ctx* c) {
@@ -1207,12 +1216,6 @@ void setup_epoch_buffers(kb2e_ctx* c) {
         c->rpar_rel_begin.alloc((size_t)c->nb * 4);
     }
     if (c->parallel() && !getenv("KB2E_NO_PREINDEX")) alloc_shadow_index(c);  // the prebuilt next-epoch index
-    c->device_bytes = 0;
-    for (DevBuf* d : {&c->ent, &c->rel, &c->w, &c->heads, &c->tails, &c->rels, &c->si_[0], &c->sj_[0], &c->side_[0],
-                      &c->si_[1], &c->sj_[1], &c->side_[1], &c->filter_slots, &c->pr_dev,
-                      &c->keys, &c->keys_sorted, &c->sort_tmp, &c->flags, &c->idx, &c->seg_start, &c->act,
-                      &c->loss, &c->xbits, &c->xreal, &c->aux, &c->aux2, &c->tickets, &c->ent_done, &c->wsnap})
-        c->device_bytes += (int64_t)d->bytes;
 }
 
 }  // namespace

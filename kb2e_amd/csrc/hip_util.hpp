@@ -34,8 +34,13 @@ inline void memset_sync(void* p, int v, size_t b) {
 }
 
 struct DevBuf {
+    // the live-byte count an allocation is charged to: the context the engine is
+    // working for (set by its entry points, kb2e_device_bytes); kept per buffer so
+    // that a free later is returned to the same context
+    static inline thread_local int64_t* tally_now = nullptr;
     void* p = nullptr;
     size_t bytes = 0;
+    int64_t* tally = nullptr;
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
@@ -43,6 +48,8 @@ struct DevBuf {
         free();
         if (b == 0) b = 16;
         HIPCHK(hipMalloc(&p, b));
+        tally = tally_now;
+        if (tally) *tally += (int64_t)b;
         // zeroed: no kernel result may depend on what an earlier engine left in the
         // heap.  hipMemset runs on the null stream, which does not order against the
         // engine's non-blocking streams: wait for it here, or an upload queued next
@@ -52,9 +59,13 @@ struct DevBuf {
         bytes = b;
     }
     void free() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            (void)hipFree(p);
+            if (tally) *tally -= (int64_t)bytes;
+        }
         p = nullptr;
         bytes = 0;
+        tally = nullptr;
     }
     template <class T>
     T* as() const { return (T*)p; }
