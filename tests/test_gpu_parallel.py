@@ -512,3 +512,20 @@ def test_transr_parallel_sub_batches_small_set(monkeypatch):
     """Sub-batches on the 30k-triple set (a hot relation of ~700 samples a batch:
     several chunks and windows a sub-batch), compat energy, n = 50."""
     _transr_vs_model(data.synthetic("small", seed=1), 50, 1, monkeypatch, St=8, compat=True, rate=0.001, sub=4)
+
+
+@pytest.mark.parametrize("model,dim,schedule,sub,want", [("R", 50, "parallel", None, 2), ("R", 64, "parallel", None, 2),
+                                                          ("R", 65, "parallel", None, 3), ("R", 100, "parallel", None, 3),
+                                                          ("R", 300, "parallel", None, 3), ("R", 50, "ordered", None, 1),
+                                                          ("E", 50, "parallel", None, 1), ("R", 50, "parallel", 1, 1),
+                                                          ("R", 100, "parallel", 4, 4)])
+def test_sub_batch_default_by_width(model, dim, schedule, sub, want):
+    """kb2e_config.sub_batches = 0 (kb2e_default_config) resolves by width at
+    kb2e_create -- 2 for PARALLEL TransR at n <= 64, 3 above, 1 elsewhere -- and
+    kb2e_get_config reports the count the context runs; an explicit count stays."""
+    ds = tiny()
+    eng = Engine(model, dim, ds.num_entities, ds.num_relations, batches=10, schedule=schedule, sub_batches=sub)
+    try:
+        assert eng.cfg.sub_batches == want
+    finally:
+        eng.close()
