@@ -131,6 +131,7 @@ struct kb2e_ctx {
     uint32_t* pin_win = nullptr;            // generator window after the epoch (31 words)
     DevBuf raw_words, glibc_starts, glibc_table, win_dev;
     int64_t nraw = 0, nraw_cap = 0;
+    int levels_cap = 0;  // next[] levels the sampler buffers hold (1, or log S for pointer doubling)
     double words_per_sample = 6.0;
     bool prefetch_valid = false;   // set cur^1 holds the stream for the current rng state
     uint64_t rng_version = 0, prefetch_version = 0;
@@ -550,11 +551,14 @@ void upload_stream(kb2e_ctx* c, int set, hipStream_t st) {
     HIPCHK(hipMemcpyAsync(c->side_[set].p, c->pin_side, c->S, hipMemcpyHostToDevice, st));
 }
 
-void ensure_sampler_capacity(kb2e_ctx* c, int64_t nraw) {
-    if (nraw <= c->nraw_cap) return;
-    const int K = std::max(1, bits_for(std::max<int64_t>(c->S - 1, 1)));
+// `doubling`: pointer doubling's K = log S levels of next[] (the fallback); the
+// chunked chain reads only next[] itself (K5: 24 levels were 7.9 GB)
+void ensure_sampler_capacity(kb2e_ctx* c, int64_t nraw, bool doubling) {
+    const int K = doubling ? std::max(1, bits_for(std::max<int64_t>(c->S - 1, 1))) : 1;
+    if (nraw <= c->nraw_cap && K <= c->levels_cap) return;
     c->words.alloc(nraw * 4);
     c->levels.alloc((size_t)K * (nraw + 1) * 4);
+    c->levels_cap = K;
     c->jfin.alloc(nraw * 4);
     c->sidefin.alloc(nraw);
     c->raw_words.alloc((nraw + GlibcRand::kDeg) * 4);
@@ -601,7 +605,8 @@ void ensure_jump_table(kb2e_ctx* c) {
 void launch_prefetch(kb2e_ctx* c) {
     const int set = c->cur ^ 1;
     const int64_t nraw = (int64_t)(c->words_per_sample * c->S) + 4096;
-    ensure_sampler_capacity(c, nraw);
+    const bool doubling = c->sampler_doubling || getenv("KB2E_SAMPLER_DOUBLING");
+    ensure_sampler_capacity(c, nraw, doubling);
     c->nraw = nraw;
     ensure_jump_table(c);
     GlibcWindow win;
@@ -642,7 +647,6 @@ void launch_prefetch(kb2e_ctx* c) {
     a.jfin = c->jfin.as<int32_t>();
     a.sidefin = c->sidefin.as<uint8_t>();
     const int64_t stride = nraw + 1;
-    const bool doubling = c->sampler_doubling || getenv("KB2E_SAMPLER_DOUBLING");
     auto launch = [&] {
         const char* sg = getenv("KB2E_SAMPLE_GRID");
         const int64_t g_full = (stride + 255) / 256;
@@ -1135,6 +1139,7 @@ void setup_epoch_buffers(kb2e_ctx* c) {
     c->prefetch_valid = false;
     c->next_pending = false;
     c->nraw_cap = 0;
+    c->levels_cap = 0;
     c->consumed_dev.alloc(16);
     if (!c->pin_consumed) HIPCHK(hipHostMalloc((void**)&c->pin_consumed, 16, 0));
     if (!c->pin_win) HIPCHK(hipHostMalloc((void**)&c->pin_win, 32 * 4, 0));
